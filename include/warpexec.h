@@ -1,0 +1,171 @@
+/*
+ * warpexec.h -- C ABI of the MI355X (gfx950) query execution layer.
+ *
+ * This is the drop-in boundary for WarpDB's execution path.  Every entry
+ * point takes plain pointers and sizes, returns a wx_status and reports
+ * failures through an (err, errlen) buffer; no C++ exception and no torch
+ * type crosses it.  Device buffers are caller-owned (hipMalloc / torch);
+ * warpexec owns only its compiled kernel cache and a per-(device, stream)
+ * workspace.
+ *
+ * Reference interfaces replaced (paths relative to the WarpDB snapshot):
+ *   wx_project_filter   jit_compile_and_launch   include/jit.hpp:7-10, src/jit.cpp:48-174
+ *                       + the launch/D2H part of WarpDB::query src/warpdb.cpp:243-256
+ *   wx_group_sum        jit_group_sum            include/jit.hpp:15-18, src/jit.cpp:179-246
+ *   wx_sort_pairs       jit_sort_pairs           include/jit.hpp:22-23, src/jit.cpp:248-281
+ *   wx_sort_float       jit_sort_float           include/jit.hpp:26-27, src/jit.cpp:283-307
+ *   wx_topk             jit_sort_float + LIMIT   src/warpdb.cpp:453-455,483-495
+ *   wx_reduce_sum       per-shard SUM of query_multi_gpu (new; the reference
+ *                       gathers dense results on the host, src/multi_gpu_utils.cpp:5-63)
+ *
+ * Expression inputs are the reference's lowered C expressions over
+ * identifiers `<column>[idx]` (include/expression.hpp:32-78), e.g.
+ * "(price[idx] * quantity[idx])".  An empty / NULL condition means no filter
+ * (src/jit.cpp:56).  The text of custom.cu (or custom_src) is prepended to
+ * every generated kernel exactly as src/jit.cpp:65-73 does.
+ *
+ * All work is enqueued on `stream` (a hipStream_t; NULL = the null stream)
+ * and is asynchronous unless WX_F_SYNC is set or a host output pointer is
+ * passed, in which case the call returns with results complete.
+ */
+#ifndef WARPEXEC_H
+#define WARPEXEC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WX_ABI_VERSION 1
+
+typedef enum wx_status {
+  WX_OK = 0,
+  WX_ERR_INVALID = 1,     /* bad argument / unknown column type / overflow */
+  WX_ERR_COMPILE = 2,     /* hiprtc failed; err holds the compiler log */
+  WX_ERR_DEVICE = 3,      /* a HIP runtime call failed */
+  WX_ERR_CAPACITY = 4,    /* an output or group table was too small */
+  WX_ERR_UNSUPPORTED = 5, /* request outside what the engine implements */
+  WX_ERR_INTERNAL = 6     /* a device-side check failed (e.g. look-back timeout) */
+} wx_status;
+
+/* Same numbering as WarpDB's DataType (include/csv_loader.hpp:13). */
+typedef enum wx_dtype {
+  WX_INT32 = 0,
+  WX_INT64 = 1,
+  WX_FLOAT32 = 2,
+  WX_FLOAT64 = 3,
+  WX_STRING = 4 /* accepted in a table, cannot be referenced by an expression */
+} wx_dtype;
+
+/* One device column: mirrors ColumnDesc (include/csv_loader.hpp:15-20);
+ * the length is the table's n_rows. */
+typedef struct wx_col {
+  const char *name;
+  int32_t dtype;
+  const void *d_ptr;
+} wx_col;
+
+/* Mirrors Table (include/csv_loader.hpp:39-51) with 64-bit row counts. */
+typedef struct wx_table {
+  int64_t n_rows;
+  int32_t n_cols;
+  const wx_col *cols;
+} wx_table;
+
+/* Where and how to run. */
+typedef struct wx_launch {
+  int32_t device;         /* HIP device ordinal */
+  void *stream;           /* hipStream_t (NULL = null stream) */
+  const char *custom_src; /* NULL: read $WARPDB_CUSTOM_PATH or ./custom.cu per call */
+  uint32_t flags;         /* WX_F_* */
+} wx_launch;
+
+#define WX_F_SYNC 1u      /* synchronise the stream and check device errors before returning */
+#define WX_F_NO_CUSTOM 2u /* do not prepend custom.cu */
+#define WX_F_TIME 4u      /* record HIP events around the main kernel (wx_timing_read) */
+
+/* wx_project_filter modes */
+#define WX_MODE_DENSE 0      /* out_vals[row] = expr where cond holds, other rows untouched (src/jit.cpp:55-61) */
+#define WX_MODE_DENSE_FILL 1 /* as DENSE, other rows set to 0.0f */
+#define WX_MODE_COMPACT 2    /* ordered stream compaction: k-th passing row -> out_vals[k], out_idx[k] */
+
+/* Project + filter.  DENSE modes write n_rows floats to d_out_vals.
+ * COMPACT writes the passing rows in ascending row order: d_out_vals[k] (nullable)
+ * and d_out_idx[k] = row_base + row (nullable; idx_bytes 4 -> int32, 8 -> int64);
+ * both must hold n_rows entries.  d_count (device int64, nullable) receives the
+ * passing count; h_count (host, nullable) too, which synchronises. */
+wx_status wx_project_filter(const wx_table *table, const char *expr, const char *cond,
+                            const wx_launch *launch, int32_t mode, float *d_out_vals,
+                            void *d_out_idx, int32_t idx_bytes, int64_t row_base,
+                            int64_t *d_count, int64_t *h_count, char *err, size_t errlen);
+
+/* SUM((float)expr) over rows where cond holds, accumulated in double.
+ * d_out (device, nullable) receives {sum as double, count as int64 bits};
+ * h_sum / h_count (host, nullable) synchronise. */
+wx_status wx_reduce_sum(const wx_table *table, const char *expr, const char *cond,
+                        const wx_launch *launch, void *d_out, double *h_sum, int64_t *h_count,
+                        char *err, size_t errlen);
+
+/* SUM((float)val_expr) GROUP BY (int)key_expr WHERE cond.  Sums in double,
+ * counts in int64, groups in ascending key order.  capacity = entries of the
+ * device outputs (and the distinct-key bound of the general-key table).
+ * Keys in [key_window_lo, key_window_lo + 4096) take the LDS fast path. */
+wx_status wx_group_sum(const wx_table *table, const char *val_expr, const char *key_expr,
+                       const char *cond, const wx_launch *launch, int32_t key_window_lo,
+                       int64_t capacity, int32_t *d_keys, double *d_sums, int64_t *d_counts,
+                       int64_t *d_n_groups, int64_t *h_n_groups, char *err, size_t errlen);
+
+/* ORDER BY order_expr [DESC] LIMIT k (1 <= k <= 256) over rows where cond
+ * holds; ties broken by ascending row index.  Outputs (device, nullable):
+ * order keys, row_base + row indices, and (float)select_expr at those rows
+ * (select_expr NULL = the order key).  The count (<= k) goes to d_count / h_count. */
+wx_status wx_topk(const wx_table *table, const char *order_expr, const char *cond,
+                  const char *select_expr, int32_t k, int32_t descending,
+                  const wx_launch *launch, int64_t row_base, float *d_keys, int64_t *d_idx,
+                  float *d_vals, int64_t *d_count, int64_t *h_count, char *err, size_t errlen);
+
+/* In-place sorts used by the legacy jit_sort_* entry points.  Stable. */
+wx_status wx_sort_pairs(int32_t *d_keys, float *d_vals, int64_t count, int32_t ascending,
+                        const wx_launch *launch, char *err, size_t errlen);
+wx_status wx_sort_float(float *d_vals, int64_t count, int32_t ascending, const wx_launch *launch,
+                        char *err, size_t errlen);
+
+/* Seeded synthetic column generator (counter-based, so every shard can
+ * generate its own rows on the device):  h = splitmix64(row + seed * 0xD1B54A32D192ED03)
+ *   kind 0: uniform float  lo + ((h >> 40) * 2^-24) * (hi - lo)   (float arithmetic)
+ *   kind 1: uniform int    lo + (h >> 32) % (hi - lo + 1)
+ * row = row_base + i; the value is converted to `dtype`. */
+wx_status wx_fill_synthetic(void *d_ptr, int32_t dtype, int64_t n, uint64_t seed,
+                            int32_t kind, double lo, double hi, int64_t row_base,
+                            const wx_launch *launch, char *err, size_t errlen);
+
+/* Build (and cache) the kernels a call would use, without launching.  Works
+ * without a GPU (arch taken from $WARPDB_ARCH, default gfx950).  op: 0 project
+ * dense, 1 project compact, 2 sum, 3 group, 4 topk.  src_out (nullable)
+ * receives the generated HIP source. */
+wx_status wx_prepare(const wx_table *table, int32_t op, const char *expr, const char *cond,
+                     const char *aux_expr, int32_t k, const wx_launch *launch, char *src_out,
+                     size_t src_len, char *err, size_t errlen);
+
+/* Synchronise `stream` and report any device-side failure flagged since the
+ * last check (look-back timeout, table capacity). */
+wx_status wx_check(const wx_launch *launch, char *err, size_t errlen);
+
+/* Sum of the HIP-event durations of the main kernels launched with WX_F_TIME
+ * on this thread since the last read (synchronises on the recorded events). */
+wx_status wx_timing_read(double *total_ms, int64_t *launches, char *err, size_t errlen);
+
+/* Kernel-cache statistics: compiled modules and hits since load. */
+void wx_cache_stats(int64_t *compiles, int64_t *hits);
+
+/* Release cached modules and workspaces of every device. */
+void wx_shutdown(void);
+
+int32_t wx_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WARPEXEC_H */

@@ -1,0 +1,362 @@
+"""GPU parity tests: the HIP path through the C ABI against the CPU oracle.
+
+Every test here calls libwarpexec.so (include/warpexec.h) with device
+buffers and compares against oracle/liboracle.so on the same seeded inputs.
+Bar: bit-exact for compaction indices, projections and double sums (the
+build uses -ffp-contract=off); order of GROUP BY / top-K results exact.
+Sizes are chosen so the oracle finishes in seconds; the 2^28-row case checks
+size-independent properties instead.
+"""
+from __future__ import annotations
+
+import os
+
+import numpy as np
+import pytest
+
+import oracle_lib as ora
+import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+from warpdb_amd import _warpexec as wx  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+DISCOUNT_SRC = "__device__ float discount(float price, float rate) {\n    return price * rate;\n}\n"
+_TD = {np.dtype(np.int32): torch.int32, np.dtype(np.int64): torch.int64,
+       np.dtype(np.float32): torch.float32, np.dtype(np.float64): torch.float64}
+
+
+def dev_table(cols, offset=0):
+    """Upload numpy columns; `offset` elements of padding make pointers unaligned."""
+    tensors = {}
+    for k, v in cols.items():
+        t = torch.empty(len(v) + offset, dtype=_TD[v.dtype], device="cuda")
+        if len(v):
+            t[offset:].copy_(torch.from_numpy(v))
+        tensors[k] = t[offset:]
+    n = len(next(iter(cols.values())))
+    dt = {torch.int32: wx.INT32, torch.int64: wx.INT64, torch.float32: wx.FLOAT32, torch.float64: wx.FLOAT64}
+    table = wx.Table(n, [wx.Column(k, dt[t.dtype], t.data_ptr() if n else 0) for k, t in tensors.items()],
+                     owners=list(tensors.values()))
+    return table, tensors
+
+
+def launch(flags=wx.F_SYNC, custom=DISCOUNT_SRC):
+    return wx.make_launch(device=0, stream=torch.cuda.current_stream().cuda_stream, custom_src=custom,
+                          flags=flags)
+
+
+def gpu_compact(table, expr, cond, idx_bytes=8, row_base=0):
+    n = table.n_rows
+    vals = torch.full((max(1, n),), float("nan"), dtype=torch.float32, device="cuda")
+    idx = torch.full((max(1, n),), -1, dtype=torch.int64 if idx_bytes == 8 else torch.int32, device="cuda")
+    cnt = wx.project_filter(table, expr, cond, launch(), wx.MODE_COMPACT, vals.data_ptr(), idx.data_ptr(),
+                            idx_bytes, row_base, want_count=True)
+    return vals[:cnt].cpu().numpy(), idx[:cnt].cpu().numpy()
+
+
+def bits(a):
+    return np.asarray(a, np.float32).view(np.uint32)
+
+
+def read_csv(path):
+    import csv
+
+    with open(path) as f:
+        r = list(csv.reader(f))
+    names = r[0]
+    return {n: np.array([float(row[i]) for row in r[1:]], np.float32) for i, n in enumerate(names)}
+
+
+# ------------------------------------------------------------------ goldens
+def load_golden():
+    import json
+
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("case", range(len(load_golden()["project"])))
+def test_golden_project(case):
+    g = load_golden()["project"][case]
+    cols = read_csv(os.path.join(GOLDEN, g["csv"]))
+    table, _ = dev_table(cols)
+    expr, cond = ora.split_where(g["query"])
+    e = ora.lower(expr)
+    c = ora.lower(cond) if cond.strip() else None
+    vals, idx = gpu_compact(table, e, c)
+    assert idx.tolist() == g["idx"]
+    assert [float.hex(float(v)) for v in vals] == [float.hex(float.fromhex(x)) for x in g["vals"]]
+
+
+def test_dense_mode_leaves_unselected_rows():
+    cols = read_csv(os.path.join(GOLDEN, "test.csv"))
+    table, _ = dev_table(cols)
+    out = torch.full((4,), -7.0, device="cuda")
+    wx.project_filter(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", launch(), wx.MODE_DENSE,
+                      out.data_ptr())
+    assert out.cpu().tolist() == [-7.0, -7.0, -7.0, 27.0]
+    wx.project_filter(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", launch(), wx.MODE_DENSE_FILL,
+                      out.data_ptr())
+    assert out.cpu().tolist() == [0.0, 0.0, 0.0, 27.0]
+    wx.project_filter(table, "(price[idx] * 0.9f)", None, launch(), wx.MODE_DENSE, out.data_ptr())
+    ref = ora.dense(ora.HostTable(cols), "price * 0.9", None, np.zeros(4, np.float32))
+    assert (bits(out.cpu().numpy()) == bits(ref)).all()
+
+
+def test_jit_arch_identity_raw_expression():
+    # tests/jit_arch_test.cpp:6-38: the un-lowered expression "price" -> 2.0
+    table, _ = dev_table({"price": np.array([2.0], np.float32), "quantity": np.array([0], np.int32)})
+    out = torch.zeros(1, device="cuda")
+    wx.project_filter(table, "price", "", launch(), wx.MODE_DENSE, out.data_ptr())
+    assert out.item() == 2.0
+    wx.project_filter(table, "price + 1", "", launch(), wx.MODE_DENSE, out.data_ptr())
+    assert out.item() == 3.0
+
+
+def test_compile_error_then_recovery():
+    # tests/jit_error_test.cpp:19-33
+    table, _ = dev_table({"price": np.array([1.5], np.float32), "quantity": np.array([2], np.int32)})
+    out = torch.zeros(1, device="cuda")
+    with pytest.raises(wx.WarpExecError) as ei:
+        wx.project_filter(table, "invalid@", "", launch(), wx.MODE_DENSE, out.data_ptr())
+    assert ei.value.status == wx.WX_ERR_COMPILE
+    assert "Kernel compilation failed" in str(ei.value)
+    wx.project_filter(table, "price + 1", "", launch(), wx.MODE_DENSE, out.data_ptr())
+    assert out.item() == 2.5
+
+
+# ------------------------------------------------------- synthetic parity
+@pytest.mark.parametrize("n", [0, 1, 5, 4095, 4096, 4097, 65536 + 3, 1_000_003])
+def test_compact_c2_shape_vs_oracle(n):
+    cols = synth.c2_table(n)
+    table, _ = dev_table(cols)
+    vals, idx = gpu_compact(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)")
+    rv, ri = ora.project_filter(ora.HostTable(cols), "price * quantity", "price > 15")
+    assert np.array_equal(idx, ri)
+    assert np.array_equal(bits(vals), bits(rv))
+
+
+@pytest.mark.parametrize("cond", ["price > 100", "price >= 0", "price > 10 AND quantity < 50",
+                                  "price < 1 OR price > 39", "quantity = 7"])
+def test_compact_selectivity_extremes(cond):
+    n = 300_001
+    cols = synth.c2_table(n)
+    table, _ = dev_table(cols)
+    vals, idx = gpu_compact(table, ora.lower("price * 0.9 + quantity"), ora.lower(cond))
+    rv, ri = ora.project_filter(ora.HostTable(cols), "price * 0.9 + quantity", cond)
+    assert np.array_equal(idx, ri)
+    assert np.array_equal(bits(vals), bits(rv))
+
+
+def test_compact_int32_index_and_row_base():
+    n = 123_457
+    cols = synth.c2_table(n, row_base=1000)
+    table, _ = dev_table(cols)
+    vals, idx = gpu_compact(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", idx_bytes=4, row_base=1000)
+    rv, ri = ora.project_filter(ora.HostTable(cols), "price * 0.9", "price > 20")
+    assert np.array_equal(idx.astype(np.int64), ri + 1000)
+    assert np.array_equal(bits(vals), bits(rv))
+
+
+def test_compact_unaligned_columns():
+    n = 100_003
+    cols = synth.c2_table(n)
+    table, _ = dev_table(cols, offset=1)
+    vals, idx = gpu_compact(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)")
+    rv, ri = ora.project_filter(ora.HostTable(cols), "price * quantity", "price > 15")
+    assert np.array_equal(idx, ri)
+    assert np.array_equal(bits(vals), bits(rv))
+
+
+def test_mixed_types_follow_jit_semantics():
+    n = 50_000
+    rng = np.random.default_rng(7)
+    cols = {
+        "a": rng.integers(-1000, 1000, n).astype(np.int32),
+        "b": rng.integers(1, 50, n).astype(np.int32),
+        "c": rng.uniform(-5, 5, n).astype(np.float64),
+        "d": rng.integers(-(1 << 40), 1 << 40, n).astype(np.int64),
+    }
+    table, _ = dev_table(cols)
+    for e_sql, e_c, c_sql, c_c in [
+        ("a / b", "(a[idx] / b[idx])", "a > 0", "(a[idx] > 0.0f)"),
+        ("c * a + 1", "((c[idx] * a[idx]) + 1.0f)", "c < 2.5", "(c[idx] < 2.5f)"),
+        ("d / 3", "(d[idx] / 3.0f)", "d != b", "(d[idx] != b[idx])"),
+    ]:
+        vals, idx = gpu_compact(table, e_c, c_c)
+        rv, ri = ora.project_filter(ora.HostTable(cols), e_sql, c_sql, sem=ora.SEM_JIT)
+        assert np.array_equal(idx, ri), e_sql
+        assert np.array_equal(bits(vals), bits(rv)), e_sql
+
+
+def test_large_compaction_properties():
+    """2^28 rows: ordering, count and values checked against torch on device."""
+    n = 1 << 28
+    price = torch.empty(n, dtype=torch.float32, device="cuda")
+    qty = torch.empty(n, dtype=torch.float32, device="cuda")
+    L = launch()
+    wx.fill_synthetic(price.data_ptr(), wx.FLOAT32, n, synth.SEED_PRICE, 0, 0.0, 40.0, L)
+    wx.fill_synthetic(qty.data_ptr(), wx.FLOAT32, n, synth.SEED_QTY, 1, 1, 100, L)
+    head = synth.c2_table(4096)
+    assert np.array_equal(price[:4096].cpu().numpy(), head["price"])
+    assert np.array_equal(qty[:4096].cpu().numpy(), head["quantity"])
+    table = wx.Table(n, [wx.Column("price", wx.FLOAT32, price.data_ptr()),
+                         wx.Column("quantity", wx.FLOAT32, qty.data_ptr())])
+    vals = torch.empty(n, dtype=torch.float32, device="cuda")
+    idx = torch.empty(n, dtype=torch.int32, device="cuda")
+    cnt = wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", L, wx.MODE_COMPACT,
+                            vals.data_ptr(), idx.data_ptr(), 4, 0, want_count=True)
+    mask = price > 15.0
+    assert cnt == int(mask.sum().item())
+    ref_idx = torch.nonzero(mask).flatten().to(torch.int32)
+    assert torch.equal(idx[:cnt], ref_idx)
+    assert torch.equal(vals[:cnt], (price * qty)[mask])
+
+
+# ------------------------------------------------------------------ SUM
+@pytest.mark.parametrize("n", [0, 3, 4096 * 7 + 1, 2_000_003])
+def test_sum_vs_oracle(n):
+    cols = synth.c2_table(n)
+    table, _ = dev_table(cols)
+    s, c = wx.reduce_sum(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", launch())
+    rs, rc = ora.reduce_sum(ora.HostTable(cols), "price * 0.9", "price > 20")
+    assert c == rc
+    assert s == rs  # float values summed in double: exact at these sizes
+
+
+# -------------------------------------------------------------- GROUP BY
+@pytest.mark.parametrize("n", [1, 1000, 2_000_003])
+def test_group_sum_c3_shape(n):
+    cols = synth.c3_table(n)
+    table, _ = dev_table(cols)
+    cap = 4096
+    keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+    sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+    g = wx.group_sum(table, "price[idx]", "quantity[idx]", None, launch(), 0, cap, keys.data_ptr(),
+                     sums.data_ptr(), cnts.data_ptr())
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity")
+    assert g == len(rk)
+    assert np.array_equal(keys[:g].cpu().numpy(), rk)
+    assert np.array_equal(sums[:g].cpu().numpy(), rs)
+    assert np.array_equal(cnts[:g].cpu().numpy(), rc)
+
+
+def test_group_sum_keys_outside_window_and_filter():
+    n = 400_000
+    rng = np.random.default_rng(11)
+    cols = {"price": synth.uniform_f32(n, 1, 0.0, 40.0),
+            "k": rng.choice(np.array([-5, -1, 0, 7, 2047, 2048, 5000, 1 << 30, -(1 << 31)], np.int32), n)}
+    table, _ = dev_table(cols)
+    cap = 64
+    keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+    sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+    for _ in range(2):  # second call checks the tables were left clean
+        g = wx.group_sum(table, "(price[idx] * 2.0f)", "k[idx]", "(price[idx] < 30.0f)", launch(), 0, cap,
+                         keys.data_ptr(), sums.data_ptr(), cnts.data_ptr())
+        rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price * 2", "k", "price < 30")
+        assert g == len(rk)
+        assert np.array_equal(keys[:g].cpu().numpy(), rk)
+        assert np.array_equal(sums[:g].cpu().numpy(), rs)
+        assert np.array_equal(cnts[:g].cpu().numpy(), rc)
+
+
+def test_group_sum_reference_golden():
+    # tests/sql_features_test.cpp:11-22 on data/test.csv: keys 2,3,4,5
+    cols = read_csv(os.path.join(GOLDEN, "test.csv"))
+    table, _ = dev_table(cols)
+    keys = torch.empty(8, dtype=torch.int32, device="cuda")
+    sums = torch.empty(8, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(8, dtype=torch.int64, device="cuda")
+    g = wx.group_sum(table, "price[idx]", "quantity[idx]", None, launch(), 0, 8, keys.data_ptr(),
+                     sums.data_ptr(), cnts.data_ptr())
+    assert g == 4
+    assert keys[:4].cpu().tolist() == [2, 3, 4, 5]
+    assert sums[:4].cpu().tolist() == [15.25, 10.5, 20.0, 30.0]
+
+
+def test_group_capacity_error():
+    cols = synth.c3_table(10_000)
+    table, _ = dev_table(cols)
+    keys = torch.empty(10, dtype=torch.int32, device="cuda")
+    sums = torch.empty(10, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(10, dtype=torch.int64, device="cuda")
+    with pytest.raises(wx.WarpExecError) as ei:
+        wx.group_sum(table, "price[idx]", "quantity[idx]", None, launch(), 0, 10, keys.data_ptr(),
+                     sums.data_ptr(), cnts.data_ptr())
+    assert ei.value.status == wx.WX_ERR_CAPACITY
+    # engine still healthy afterwards
+    big = torch.empty(2048, dtype=torch.int32, device="cuda")
+    bs = torch.empty(2048, dtype=torch.float64, device="cuda")
+    bc = torch.empty(2048, dtype=torch.int64, device="cuda")
+    g = wx.group_sum(table, "price[idx]", "quantity[idx]", None, launch(), 0, 2048, big.data_ptr(),
+                     bs.data_ptr(), bc.data_ptr())
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity")
+    assert g == len(rk) and np.array_equal(bs[:g].cpu().numpy(), rs)
+
+
+# ---------------------------------------------------------------- top-K
+@pytest.mark.parametrize("k,desc", [(5, True), (1, True), (5, False), (32, True)])
+def test_topk_vs_oracle(k, desc):
+    n = 1_000_003
+    cols = synth.c2_table(n)
+    table, _ = dev_table(cols)
+    keys = torch.empty(k, device="cuda")
+    idx = torch.empty(k, dtype=torch.int64, device="cuda")
+    vals = torch.empty(k, device="cuda")
+    m = wx.topk(table, "price[idx]", None, "discount(price[idx], 0.9f)", k, desc, launch(), keys.data_ptr(),
+                idx.data_ptr(), vals.data_ptr())
+    rk, ri, rv = ora.topk(ora.HostTable(cols), "price", k, desc, select_expr="discount(price, 0.9)")
+    assert m == len(rk)
+    assert np.array_equal(bits(keys[:m].cpu().numpy()), bits(rk))
+    assert np.array_equal(idx[:m].cpu().numpy(), ri)
+    assert np.array_equal(bits(vals[:m].cpu().numpy()), bits(rv))
+
+
+def test_topk_ties_and_filter():
+    n = 200_000
+    cols = {"price": np.floor(synth.uniform_f32(n, 1, 0.0, 40.0)).astype(np.float32),
+            "quantity": synth.uniform_int(n, 2, 1, 100).astype(np.float32)}
+    table, _ = dev_table(cols)
+    k = 7
+    keys = torch.empty(k, device="cuda")
+    idx = torch.empty(k, dtype=torch.int64, device="cuda")
+    m = wx.topk(table, "(price[idx] + quantity[idx])", "(quantity[idx] < 50.0f)", None, k, True, launch(),
+                keys.data_ptr(), idx.data_ptr())
+    rk, ri, _ = ora.topk(ora.HostTable(cols), "price + quantity", k, True, cond="quantity < 50")
+    assert m == k
+    assert np.array_equal(idx[:m].cpu().numpy(), ri)
+    assert np.array_equal(keys[:m].cpu().numpy(), rk)
+
+
+def test_topk_fewer_rows_than_k():
+    cols = read_csv(os.path.join(GOLDEN, "test.csv"))
+    table, _ = dev_table(cols)
+    keys = torch.empty(5, device="cuda")
+    m = wx.topk(table, "price[idx]", None, None, 5, True, launch(), keys.data_ptr())
+    assert m == 4
+    assert keys[:4].cpu().tolist() == [30.0, 20.0, 15.25, 10.5]  # SURVEY.md 8c, C5 golden
+
+
+# ----------------------------------------------------------------- sorts
+@pytest.mark.parametrize("n", [1, 17, 2048, 5000, 70_000])
+def test_sort_float_and_pairs(n):
+    rng = np.random.default_rng(n)
+    v = np.round(rng.uniform(-100, 100, n), 1).astype(np.float32)
+    for asc in (True, False):
+        t = torch.from_numpy(v.copy()).cuda()
+        wx.sort_float(t.data_ptr(), n, asc, launch())
+        ref = np.sort(v) if asc else -np.sort(-v)
+        assert np.array_equal(t.cpu().numpy(), ref)
+    keys = rng.integers(-50, 50, n).astype(np.int32)
+    for asc in (True, False):
+        tk = torch.from_numpy(keys.copy()).cuda()
+        tv = torch.from_numpy(v.copy()).cuda()
+        wx.sort_pairs(tk.data_ptr(), tv.data_ptr(), n, asc, launch())
+        order = np.argsort(keys if asc else -keys.astype(np.int64), kind="stable")
+        assert np.array_equal(tk.cpu().numpy(), keys[order])
+        assert np.array_equal(tv.cpu().numpy(), v[order])

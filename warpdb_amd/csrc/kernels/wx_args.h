@@ -1,0 +1,153 @@
+// wx_args.h -- kernel argument blocks shared by the host runtime
+// (warpexec.cpp includes this file) and the device templates (warpexec
+// prepends the same text to every hiprtc program), so the two layouts can
+// never drift.  Plain C++ only: no host or device headers.
+#ifndef WX_ARGS_H
+#define WX_ARGS_H
+
+typedef unsigned long long wx_u64;
+typedef long long wx_i64;
+typedef unsigned int wx_u32;
+
+#define WX_MAX_COLS 16
+#define WX_BLOCK 256
+#define WX_WAVES (WX_BLOCK / 64)
+
+// device-side error bits, OR-ed into the workspace counter word ctrs[1]
+#define WX_DEVERR_LOOKBACK 1u
+#define WX_DEVERR_CAPACITY 2u
+#define WX_DEVERR_UNSUPPORTED 4u
+
+#define WX_OP_DENSE 0
+#define WX_OP_COMPACT 1
+#define WX_OP_SUM 2
+#define WX_OP_GROUP 3
+#define WX_OP_TOPK 4
+#define WX_OP_UTIL 5
+
+#define WX_COMPACT_GROUPS 4
+#define WX_COMPACT_TILE (WX_BLOCK * 4 * WX_COMPACT_GROUPS)
+#define WX_GROUP_WINDOW 2048
+#define WX_GROUP_HSORT_MAX 4096
+#define WX_TOPK_MAX 32
+#define WX_SORT_LDS (WX_BLOCK * 8)
+
+struct WxDenseArgs {
+  const void *col[WX_MAX_COLS];
+  float *out;
+  wx_i64 n_rows;
+  int fill;
+};
+
+struct WxCompactArgs {
+  const void *col[WX_MAX_COLS];
+  float *out_val;     // nullable
+  void *out_idx;      // nullable; int32 or int64
+  wx_u64 *status;     // [n_tiles], zeroed per call
+  wx_u64 *ctrs;       // [0] tile ticket (zeroed per call), [1] error bits
+  wx_i64 *count_out;  // nullable
+  wx_i64 n_rows;
+  wx_i64 n_tiles;
+  wx_i64 row_base;
+  int idx64;
+};
+
+struct WxSumArgs {
+  const void *col[WX_MAX_COLS];
+  double *part_sum;  // [gridDim.x]
+  wx_i64 *part_cnt;  // [gridDim.x]
+  wx_i64 n_rows;
+};
+
+struct WxGroupArgs {
+  const void *col[WX_MAX_COLS];
+  wx_i64 n_rows;
+  double *win_sum;  // [WX_GROUP_WINDOW]
+  wx_u64 *win_cnt;  // [WX_GROUP_WINDOW]
+  wx_u64 *h_tag;    // [hcap] 0 = empty, else (u32)key | 1<<32
+  double *h_sum;    // [hcap]
+  wx_u64 *h_cnt;    // [hcap]
+  wx_u32 *h_used;   // [hcap] slots taken, in insertion order
+  wx_u64 *ctrs;     // [0] used slots, [1] error bits
+  wx_u32 hmask;     // hcap - 1 (hcap a power of two)
+  int key_lo;
+};
+
+struct WxGroupFinArgs {
+  double *win_sum;
+  wx_u64 *win_cnt;
+  wx_u64 *h_tag;
+  double *h_sum;
+  wx_u64 *h_cnt;
+  wx_u32 *h_used;
+  wx_u64 *ctrs;
+  int *out_keys;
+  double *out_sums;
+  wx_i64 *out_counts;
+  wx_i64 *n_groups_out;
+  wx_i64 capacity;
+  int key_lo;
+};
+
+struct WxTopkArgs {
+  const void *col[WX_MAX_COLS];
+  wx_u32 *cand_k;  // [gridDim.x * K]
+  wx_i64 *cand_i;  // [gridDim.x * K]
+  wx_i64 n_rows;
+};
+
+struct WxTopkFinArgs {
+  const void *col[WX_MAX_COLS];
+  const wx_u32 *cand_k;
+  const wx_i64 *cand_i;
+  wx_i64 n_cand;
+  wx_i64 row_base;
+  float *out_keys;
+  wx_i64 *out_idx;
+  float *out_vals;
+  wx_i64 *count_out;
+};
+
+struct WxFillArgs {
+  void *out;
+  wx_i64 n;
+  wx_u64 seed;
+  double lo, hi;
+  wx_i64 row_base;
+  int dtype;
+  int kind;
+};
+
+struct WxSortPrepArgs {
+  const void *src;
+  wx_u64 *keys;
+  wx_i64 n;
+  wx_i64 npad;
+  int kind;  // 0 float values, 1 int keys
+  int ascending;
+};
+
+struct WxSortPassArgs {
+  wx_u64 *keys;
+  wx_i64 npad;
+  wx_i64 k;
+  wx_i64 j;  // global pass: partner distance; LDS pass: kend
+};
+
+struct WxSortApplyArgs {
+  const wx_u64 *keys;
+  wx_i64 n;
+  const void *src_a;
+  void *dst_a;
+  const float *src_v;
+  float *dst_v;
+};
+
+struct WxSumFinArgs {
+  const double *part_sum;
+  const wx_i64 *part_cnt;
+  double *out;  // {sum, count bits}
+  int n_parts;
+};
+
+#endif  // WX_ARGS_H

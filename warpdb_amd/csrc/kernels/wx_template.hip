@@ -1,0 +1,844 @@
+// wx_template.hip -- hand-written gfx950 kernel templates for the WarpDB
+// execution path.  warpexec prepends custom.cu (src/jit.cpp:65-73) and a
+// generated prelude, then compiles the result with hiprtc for the device's
+// arch.  The prelude defines:
+//   WX_OP          which kernel family to instantiate (see WX_OP_* below)
+//   WX_COLS(X)     X(name, c_type, slot) for every column the expressions use
+//   WX_EXPR        projection / SUM value / GROUP BY value / ORDER BY key
+//   WX_HAS_COND, WX_COND     optional WHERE predicate
+//   WX_KEY         GROUP BY key expression
+//   WX_HAS_SELECT, WX_SELECT top-K output expression (evaluated by gather)
+//   WX_TOPK_K, WX_TOPK_DESC  top-K size and direction
+//   WX_ALIGNED16   1 when every column / output pointer is 16-byte aligned
+// Expressions are the reference's lowered strings ("price[idx] * 2.0f",
+// include/expression.hpp:32-78): a column name is bound either to a register
+// value with operator[] (streaming kernels) or to the column pointer (gather).
+//
+// The design is HBM-streaming: 256-thread workgroups (4 wave64s), 16-byte
+// loads per lane (one 1 KiB access per wave-instruction), everything else
+// kept in registers / LDS.  MFMA is not used: nothing here is a contraction.
+
+#ifndef WX_ALIGNED16
+#define WX_ALIGNED16 0
+#endif
+#ifndef WX_HAS_COND
+#define WX_HAS_COND 0
+#endif
+#ifndef WX_COLS
+#define WX_COLS(X)
+#endif
+
+namespace wx {
+
+// A column value bound in registers: `price[idx]` and plain `price` both read it.
+template <typename T>
+struct reg {
+  T v;
+  __device__ __forceinline__ T operator[](wx_i64) const { return v; }
+  __device__ __forceinline__ operator T() const { return v; }
+};
+
+// Four consecutive rows [r0, r0+4) of one column into registers.  Full,
+// aligned groups use 16-byte loads (global_load_dwordx4); the ragged tail
+// falls back to guarded scalar loads and zero-fills.
+template <typename T>
+__device__ __forceinline__ void load4(const void *base, wx_i64 r0, wx_i64 n, T (&o)[4]) {
+  const T *p = static_cast<const T *>(base);
+  if (WX_ALIGNED16 && r0 + 4 <= n) {
+    if constexpr (sizeof(T) == 4) {
+      typedef T v4 __attribute__((ext_vector_type(4)));
+      const v4 x = *reinterpret_cast<const v4 *>(p + r0);
+      o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
+    } else {
+      typedef T v2 __attribute__((ext_vector_type(2)));
+      const v2 x = *reinterpret_cast<const v2 *>(p + r0);
+      const v2 y = *reinterpret_cast<const v2 *>(p + r0 + 2);
+      o[0] = x.x; o[1] = x.y; o[2] = y.x; o[3] = y.y;
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (r0 + e < n) ? p[r0 + e] : T(0);
+  }
+}
+
+__device__ __forceinline__ wx_u64 ld_agent(const wx_u64 *p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st_agent(wx_u64 *p, wx_u64 v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+__device__ __forceinline__ wx_u32 lanes_below(wx_u64 m) {
+  return __builtin_amdgcn_mbcnt_hi((wx_u32)(m >> 32), __builtin_amdgcn_mbcnt_lo((wx_u32)m, 0u));
+}
+
+__device__ __forceinline__ wx_u64 wave_sum_u64(wx_u64 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+__device__ __forceinline__ double wave_sum_f64(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  return v;
+}
+
+// Order-preserving float -> u32 map used by the top-K and sort kernels.
+// -0.0 is canonicalised to +0.0 (they compare equal on the CPU); NaN maps to
+// 0, below every number.
+__device__ __forceinline__ wx_u32 f2ord(float f) {
+  if (f != f) return 0u;
+  if (f == 0.0f) f = 0.0f;
+  const wx_u32 u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+__device__ __forceinline__ float ord2f(wx_u32 m) {
+  if (m == 0u) return __uint_as_float(0x7fc00000u);
+  const wx_u32 u = (m & 0x80000000u) ? (m & 0x7fffffffu) : ~m;
+  return __uint_as_float(u);
+}
+
+}  // namespace wx
+
+// ---------------------------------------------------------------------------
+// Expression binding helpers.  Every identifier in the scope of an evaluated
+// expression that is not a column carries a wx_ prefix so user column names
+// cannot collide with it.
+#define WX_DECL_LOAD(name, T, slot) \
+  T wx_v##slot[4];                  \
+  ::wx::load4<T>(wx_a.col[slot], wx_r0, wx_a.n_rows, wx_v##slot);
+#define WX_BIND_REG(name, T, slot) const ::wx::reg<T> name{wx_v##slot[wx_e]};
+#define WX_BIND_PTR(name, T, slot) const T *__restrict__ name = static_cast<const T *>(wx_a.col[slot]);
+
+#if WX_HAS_COND
+#define WX_EVAL_COND() static_cast<bool>(WX_COND)
+#else
+#define WX_EVAL_COND() true
+#endif
+
+// ===========================================================================
+#if WX_OP == WX_OP_DENSE
+// Dense projection (the reference contract, src/jit.cpp:55-61):
+// out[row] = expr where cond holds.  fill = 1 also writes 0.0f elsewhere.
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseArgs wx_a) {
+  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
+  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 wx_q = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q < wx_nq; wx_q += wx_stride) {
+    const wx_i64 wx_r0 = wx_q << 2;
+    WX_COLS(WX_DECL_LOAD)
+    float wx_o[4];
+    bool wx_k[4];
+#pragma unroll
+    for (int wx_e = 0; wx_e < 4; ++wx_e) {
+      WX_COLS(WX_BIND_REG)
+      const wx_i64 idx = wx_r0 + wx_e;
+      (void)idx;
+      wx_k[wx_e] = WX_EVAL_COND();
+      wx_o[wx_e] = static_cast<float>(WX_EXPR);
+    }
+    if (wx_a.fill && WX_ALIGNED16 && wx_r0 + 4 <= wx_a.n_rows) {
+      typedef float f4 __attribute__((ext_vector_type(4)));
+      f4 v;
+      v.x = wx_k[0] ? wx_o[0] : 0.0f;
+      v.y = wx_k[1] ? wx_o[1] : 0.0f;
+      v.z = wx_k[2] ? wx_o[2] : 0.0f;
+      v.w = wx_k[3] ? wx_o[3] : 0.0f;
+      *reinterpret_cast<f4 *>(wx_a.out + wx_r0) = v;
+    } else {
+#pragma unroll
+      for (int wx_e = 0; wx_e < 4; ++wx_e)
+        if (wx_r0 + wx_e < wx_a.n_rows && (wx_k[wx_e] || wx_a.fill))
+          wx_a.out[wx_r0 + wx_e] = wx_k[wx_e] ? wx_o[wx_e] : 0.0f;
+    }
+  }
+}
+#endif
+
+// ===========================================================================
+#if WX_OP == WX_OP_COMPACT
+// Ordered stream compaction, single pass with decoupled look-back.
+//
+// Tile = 256 threads x WX_GROUPS groups x 4 rows.  Row (g, thread, e) of a
+// tile sits at offset g*1024 + thread*4 + e, so every group is one 16-byte
+// load per lane per column.  In-tile ranks come from wavefront ballots
+// (v_mbcnt) and a 4-wave x WX_GROUPS LDS table; the tile's global offset from
+// the predecessors' 8-byte status words {flag:2 | value:62}.  A status word
+// is its own payload (written and read by single agent-scope 8-byte atomics),
+// so no fence is needed; output rows are never read inside the launch.
+// Tiles are taken in order from a ticket counter, so every predecessor of a
+// tile is already resident: the look-back always terminates.
+#define WX_GROUPS WX_COMPACT_GROUPS
+#define WX_TILE WX_COMPACT_TILE
+#define WX_FLAG_A (1ull << 62)
+#define WX_FLAG_P (2ull << 62)
+#define WX_VAL_MASK ((1ull << 62) - 1ull)
+#ifndef WX_SPIN_LIMIT
+#define WX_SPIN_LIMIT (1u << 24)
+#endif
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_compact(WxCompactArgs wx_a) {
+  __shared__ wx_u32 s_wave_cnt[WX_WAVES][WX_GROUPS];
+  __shared__ wx_i64 s_excl;
+  __shared__ wx_u32 s_tile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  if (tid == 0)
+    s_tile = (wx_u32)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const wx_i64 tile = s_tile;
+  const wx_i64 tile_base = tile * WX_TILE;
+
+  bool wx_keep[WX_GROUPS][4];
+  float wx_val[WX_GROUPS][4];
+#pragma unroll
+  for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
+    const wx_i64 wx_r0 = tile_base + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)tid * 4;
+    WX_COLS(WX_DECL_LOAD)
+#pragma unroll
+    for (int wx_e = 0; wx_e < 4; ++wx_e) {
+      WX_COLS(WX_BIND_REG)
+      const wx_i64 idx = wx_r0 + wx_e;
+      bool wx_k = idx < wx_a.n_rows;
+      wx_k = wx_k && WX_EVAL_COND();
+      wx_keep[wx_g][wx_e] = wx_k;
+      wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
+    }
+  }
+
+  // In-tile ranks: per (group, e) one 64-bit ballot.
+  wx_u32 lane_pre[WX_GROUPS];
+#pragma unroll
+  for (int g = 0; g < WX_GROUPS; ++g) {
+    wx_u32 pre = 0, tot = 0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const wx_u64 m = __builtin_amdgcn_ballot_w64(wx_keep[g][e]);
+      pre += wx::lanes_below(m);
+      tot += (wx_u32)__builtin_popcountll(m);
+    }
+    lane_pre[g] = pre;
+    if (lane == 0) s_wave_cnt[wave][g] = tot;
+  }
+  __syncthreads();
+
+  wx_u32 grp_base[WX_GROUPS];
+  wx_u32 block_total = 0;
+#pragma unroll
+  for (int g = 0; g < WX_GROUPS; ++g) {
+    wx_u32 before = 0, gsum = 0;
+#pragma unroll
+    for (int w = 0; w < WX_WAVES; ++w) {
+      const wx_u32 c = s_wave_cnt[w][g];
+      before += (w < wave) ? c : 0u;
+      gsum += c;
+    }
+    grp_base[g] = block_total + before;
+    block_total += gsum;
+  }
+
+  // Decoupled look-back (wave 0).
+  if (wave == 0) {
+    wx_i64 excl = 0;
+    if (tile == 0) {
+      if (lane == 0) wx::st_agent(&wx_a.status[0], WX_FLAG_P | (wx_u64)block_total);
+    } else {
+      if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_A | (wx_u64)block_total);
+      wx_i64 look = tile - 1;
+      wx_u32 spins = 0;
+      while (true) {
+        const wx_i64 t = look - lane;
+        wx_u64 s = WX_FLAG_P;  // "tile -1": inclusive prefix 0
+        if (t >= 0) {
+          s = wx::ld_agent(&wx_a.status[t]);
+          while ((s >> 62) == 0ull) {
+            __builtin_amdgcn_s_sleep(1);
+            s = wx::ld_agent(&wx_a.status[t]);
+            if (++spins > WX_SPIN_LIMIT) {
+              atomicOr(reinterpret_cast<unsigned int *>(&wx_a.ctrs[1]), WX_DEVERR_LOOKBACK);
+              s = WX_FLAG_P;
+            }
+          }
+        }
+        const wx_u64 pmask = __builtin_amdgcn_ballot_w64((s >> 62) == 2ull);
+        wx_u64 v = s & WX_VAL_MASK;
+        if (pmask) {
+          const int first = __builtin_ctzll(pmask);
+          v = (lane <= first) ? v : 0ull;
+          excl += (wx_i64)wx::wave_sum_u64(v);
+          break;
+        }
+        excl += (wx_i64)wx::wave_sum_u64(v);
+        look -= 64;
+      }
+      if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_P | (wx_u64)(excl + block_total));
+    }
+    if (lane == 0) s_excl = excl;
+  }
+  __syncthreads();
+  const wx_i64 excl = s_excl;
+
+#pragma unroll
+  for (int g = 0; g < WX_GROUPS; ++g) {
+    const wx_i64 r0 = tile_base + (wx_i64)g * (WX_BLOCK * 4) + (wx_i64)tid * 4;
+    wx_i64 pos = excl + grp_base[g] + lane_pre[g];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (wx_keep[g][e]) {
+        if (wx_a.out_val) wx_a.out_val[pos] = wx_val[g][e];
+        if (wx_a.out_idx) {
+          const wx_i64 gi = wx_a.row_base + r0 + e;
+          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
+          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
+        }
+        ++pos;
+      }
+    }
+  }
+  if (tid == 0 && tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
+}
+#endif
+
+// ===========================================================================
+#if WX_OP == WX_OP_SUM
+// SUM((float)expr) WHERE cond in double.  Persistent grid-stride pass with
+// WX_UNROLL row quads in flight per thread; one partial per block, combined
+// in a fixed order by wx_sum_finalize (bitwise reproducible).
+#ifndef WX_UNROLL
+#define WX_UNROLL 4
+#endif
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_reduce_sum(WxSumArgs wx_a) {
+  __shared__ double s_sum[WX_WAVES];
+  __shared__ wx_i64 s_cnt[WX_WAVES];
+  double wx_acc = 0.0;
+  wx_i64 wx_cnt = 0;
+  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
+  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq; wx_q0 += wx_stride * WX_UNROLL) {
+#pragma unroll
+    for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+      const wx_i64 wx_q = wx_q0 + wx_u * wx_stride;
+      if (wx_q < wx_nq) {
+        const wx_i64 wx_r0 = wx_q << 2;
+        WX_COLS(WX_DECL_LOAD)
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e) {
+          WX_COLS(WX_BIND_REG)
+          const wx_i64 idx = wx_r0 + wx_e;
+          const bool wx_k = idx < wx_a.n_rows && WX_EVAL_COND();
+          const float wx_val = static_cast<float>(WX_EXPR);
+          wx_acc += wx_k ? (double)wx_val : 0.0;
+          wx_cnt += wx_k ? 1 : 0;
+        }
+      }
+    }
+  }
+  double acc = wx::wave_sum_f64(wx_acc);
+  wx_i64 cnt = (wx_i64)wx::wave_sum_u64((wx_u64)wx_cnt);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { s_sum[wave] = acc; s_cnt[wave] = cnt; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s = 0.0;
+    wx_i64 c = 0;
+    for (int w = 0; w < WX_WAVES; ++w) { s += s_sum[w]; c += s_cnt[w]; }
+    wx_a.part_sum[blockIdx.x] = s;
+    wx_a.part_cnt[blockIdx.x] = c;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sum_finalize(WxSumFinArgs a) {
+  __shared__ double s_sum[WX_BLOCK];
+  __shared__ wx_i64 s_cnt[WX_BLOCK];
+  double s = 0.0;
+  wx_i64 c = 0;
+  for (int i = threadIdx.x; i < a.n_parts; i += WX_BLOCK) { s += a.part_sum[i]; c += a.part_cnt[i]; }
+  s_sum[threadIdx.x] = s;
+  s_cnt[threadIdx.x] = c;
+  __syncthreads();
+  for (int w = WX_BLOCK / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) { s_sum[threadIdx.x] += s_sum[threadIdx.x + w]; s_cnt[threadIdx.x] += s_cnt[threadIdx.x + w]; }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    a.out[0] = s_sum[0];
+    reinterpret_cast<wx_i64 *>(a.out)[1] = s_cnt[0];
+  }
+}
+#endif
+
+// ===========================================================================
+#if WX_OP == WX_OP_GROUP
+// GROUP BY SUM: two-stage reduction.  Stage 1 privatises a dense key window
+// [key_lo, key_lo + WX_GWIN) in LDS (ds_add_f64 / ds_add_u32 per row), then
+// flushes non-empty bins to global accumulators with one global_atomic_add_f64
+// per bin per block.  Keys outside the window go to a global open-addressing
+// table (agent-scope CAS).  wx_group_finalize emits groups in ascending key
+// order and returns every accumulator it used to zero, so the next call needs
+// no memset.  Sums of float values in double are exact (hence order-free)
+// while every partial sum stays below 2^53 ulps of the smallest value.
+#define WX_GWIN WX_GROUP_WINDOW
+#ifndef WX_UNROLL
+#define WX_UNROLL 2
+#endif
+#define WX_HSORT_MAX WX_GROUP_HSORT_MAX
+
+__device__ __forceinline__ void wx_hash_add(const WxGroupArgs &a, int key, double v) {
+  const wx_u64 tag = (wx_u64)(wx_u32)key | (1ull << 32);
+  wx_u32 h = ((wx_u32)key * 2654435761u) & a.hmask;
+  for (wx_u32 probe = 0; probe <= a.hmask; ++probe) {
+    wx_u64 cur = wx::ld_agent(&a.h_tag[h]);
+    if (cur == 0ull) {
+      const wx_u64 prev = atomicCAS(&a.h_tag[h], 0ull, tag);
+      if (prev == 0ull) {
+        const wx_u64 u = __hip_atomic_fetch_add(&a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.h_used[u] = h;
+        cur = tag;
+      } else {
+        cur = prev;
+      }
+    }
+    if (cur == tag) {
+      atomicAdd(&a.h_sum[h], v);
+      atomicAdd(&a.h_cnt[h], 1ull);
+      return;
+    }
+    h = (h + 1) & a.hmask;
+  }
+  atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_CAPACITY);
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs wx_a) {
+  __shared__ double wx_s_sum[WX_GWIN];
+  __shared__ wx_u32 wx_s_cnt[WX_GWIN];
+  for (int i = threadIdx.x; i < WX_GWIN; i += WX_BLOCK) { wx_s_sum[i] = 0.0; wx_s_cnt[i] = 0u; }
+  __syncthreads();
+  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
+  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq; wx_q0 += wx_stride * WX_UNROLL) {
+#pragma unroll
+    for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+      const wx_i64 wx_q = wx_q0 + wx_u * wx_stride;
+      if (wx_q < wx_nq) {
+        const wx_i64 wx_r0 = wx_q << 2;
+        WX_COLS(WX_DECL_LOAD)
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e) {
+          WX_COLS(WX_BIND_REG)
+          const wx_i64 idx = wx_r0 + wx_e;
+          if (idx < wx_a.n_rows && WX_EVAL_COND()) {
+            const int wx_key = static_cast<int>(WX_KEY);
+            const float wx_val = static_cast<float>(WX_EXPR);
+            const wx_u32 wx_bin = (wx_u32)(wx_key - wx_a.key_lo);
+            if (wx_bin < (wx_u32)WX_GWIN) {
+              atomicAdd(&wx_s_sum[wx_bin], (double)wx_val);
+              atomicAdd(&wx_s_cnt[wx_bin], 1u);
+            } else {
+              wx_hash_add(wx_a, wx_key, (double)wx_val);
+            }
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < WX_GWIN; i += WX_BLOCK) {
+    const wx_u32 c = wx_s_cnt[i];
+    if (c) {
+      atomicAdd(&wx_a.win_sum[i], wx_s_sum[i]);
+      atomicAdd(&wx_a.win_cnt[i], (wx_u64)c);
+    }
+  }
+}
+
+// One block: sort the general-key entries, merge with the dense window in
+// ascending key order, write the outputs, zero what was used.
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroupFinArgs a) {
+  __shared__ wx_u64 s_ent[WX_HSORT_MAX];  // (key ^ sign) << 32 | used-list position
+  __shared__ wx_u32 s_scan[WX_BLOCK];
+  __shared__ wx_i64 s_nlo;
+  const int tid = threadIdx.x;
+  const wx_i64 n_hash = (wx_i64)a.ctrs[0];
+  const bool too_many = n_hash > WX_HSORT_MAX;
+  if (too_many) {
+    if (tid == 0) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_UNSUPPORTED);
+  }
+  const int nh = too_many ? 0 : (int)n_hash;
+  int npad = 1;
+  while (npad < nh) npad <<= 1;
+  for (int i = tid; i < npad; i += WX_BLOCK) {
+    wx_u64 e = ~0ull;
+    if (i < nh) {
+      const wx_u32 slot = a.h_used[i];
+      const wx_u32 key = (wx_u32)a.h_tag[slot];
+      e = ((wx_u64)(key ^ 0x80000000u) << 32) | (wx_u32)i;
+    }
+    s_ent[i] = e;
+  }
+  __syncthreads();
+  for (int k = 2; k <= npad; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < npad; i += WX_BLOCK) {
+        const int p = i ^ j;
+        if (p > i) {
+          const wx_u64 x = s_ent[i], y = s_ent[p];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) { s_ent[i] = y; s_ent[p] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  // number of hash keys below the window
+  if (tid == 0) {
+    wx_i64 c = 0;
+    while (c < nh && (int)((wx_u32)(s_ent[c] >> 32) ^ 0x80000000u) < a.key_lo) ++c;
+    s_nlo = c;
+  }
+  __syncthreads();
+  const wx_i64 nlo = s_nlo;
+  // dense window compaction (ascending bins), block-wide scan in chunks
+  wx_i64 out_pos = nlo;
+  for (int base = 0; base < WX_GWIN; base += WX_BLOCK) {
+    const int b = base + tid;
+    const wx_u64 c = (b < WX_GWIN) ? a.win_cnt[b] : 0ull;
+    const wx_u32 f = c ? 1u : 0u;
+    s_scan[tid] = f;
+    __syncthreads();
+    for (int o = 1; o < WX_BLOCK; o <<= 1) {
+      const wx_u32 t = (tid >= o) ? s_scan[tid - o] : 0u;
+      __syncthreads();
+      s_scan[tid] += t;
+      __syncthreads();
+    }
+    const wx_i64 pos = out_pos + s_scan[tid] - f;
+    if (f && pos < a.capacity) {
+      a.out_keys[pos] = a.key_lo + b;
+      a.out_sums[pos] = a.win_sum[b];
+      a.out_counts[pos] = (wx_i64)c;
+    }
+    if (b < WX_GWIN && c) { a.win_sum[b] = 0.0; a.win_cnt[b] = 0ull; }
+    out_pos += s_scan[WX_BLOCK - 1];
+    __syncthreads();
+  }
+  // hash entries: below-window ones first, the rest after the window
+  for (int i = tid; i < nh; i += WX_BLOCK) {
+    const wx_u64 e = s_ent[i];
+    const wx_u32 slot = a.h_used[(wx_u32)e];
+    const wx_i64 pos = (i < nlo) ? (wx_i64)i : out_pos + (i - nlo);
+    if (pos < a.capacity) {
+      a.out_keys[pos] = (int)((wx_u32)(e >> 32) ^ 0x80000000u);
+      a.out_sums[pos] = a.h_sum[slot];
+      a.out_counts[pos] = (wx_i64)a.h_cnt[slot];
+    }
+  }
+  __syncthreads();
+  const wx_i64 total = out_pos + (nh - nlo);
+  // return the general-key table to its clean state
+  for (wx_i64 i = tid; i < n_hash; i += WX_BLOCK) {
+    const wx_u32 slot = a.h_used[i];
+    a.h_tag[slot] = 0ull;
+    a.h_sum[slot] = 0.0;
+    a.h_cnt[slot] = 0ull;
+  }
+  if (tid == 0) {
+    a.ctrs[0] = 0ull;
+    *a.n_groups_out = too_many ? -1 : total;
+    if (total > a.capacity) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_CAPACITY);
+  }
+}
+#endif
+
+// ===========================================================================
+#if WX_OP == WX_OP_TOPK
+// ORDER BY key [DESC] LIMIT K.  Each lane keeps its K best (ord, row) pairs
+// sorted in registers; a row costs one compare against the lane's worst
+// entry unless it enters.  Lanes merge by K rounds of a wave64 arg-max
+// (butterfly shuffles), waves merge through LDS, and blocks emit K
+// candidates each; wx_topk_finalize repeats the merge over all candidates and
+// evaluates the SELECT expression at the winning rows (gather binding).
+// Total order: better key first, then smaller row index.
+#ifndef WX_TOPK_K
+#define WX_TOPK_K 5
+#endif
+#ifndef WX_TOPK_DESC
+#define WX_TOPK_DESC 1
+#endif
+#ifndef WX_UNROLL
+#define WX_UNROLL 4
+#endif
+#define WX_IDX_NONE 0x7fffffffffffffffll
+
+namespace wx {
+// map so that "larger is better" in both directions; NaN (0) stays worst
+__device__ __forceinline__ wx_u32 rank_of(float f) {
+  const wx_u32 m = f2ord(f);
+  if (WX_TOPK_DESC || m == 0u) return m;
+  return ~m;  // ascending: smaller float = better; m != 0 so ~m != 0xffffffff unless m == 0
+}
+__device__ __forceinline__ float key_of(wx_u32 r) { return ord2f((WX_TOPK_DESC || r == 0u) ? r : ~r); }
+__device__ __forceinline__ bool better(wx_u32 ka, wx_i64 ia, wx_u32 kb, wx_i64 ib) {
+  return ka > kb || (ka == kb && ia < ib);
+}
+
+struct TopList {
+  wx_u32 k[WX_TOPK_K];
+  wx_i64 i[WX_TOPK_K];
+  __device__ __forceinline__ void init() {
+#pragma unroll
+    for (int j = 0; j < WX_TOPK_K; ++j) { k[j] = 0u; i[j] = WX_IDX_NONE; }
+  }
+  __device__ __forceinline__ void push(wx_u32 key, wx_i64 idx) {
+    if (!better(key, idx, k[WX_TOPK_K - 1], i[WX_TOPK_K - 1])) return;
+    bool done = false;
+#pragma unroll
+    for (int j = WX_TOPK_K - 1; j >= 0; --j) {
+      if (!done) {
+        if (j == 0 || !better(key, idx, k[j - 1], i[j - 1])) {
+          k[j] = key; i[j] = idx; done = true;
+        } else {
+          k[j] = k[j - 1]; i[j] = i[j - 1];
+        }
+      }
+    }
+  }
+  __device__ __forceinline__ void pop() {
+#pragma unroll
+    for (int j = 0; j < WX_TOPK_K - 1; ++j) { k[j] = k[j + 1]; i[j] = i[j + 1]; }
+    k[WX_TOPK_K - 1] = 0u;
+    i[WX_TOPK_K - 1] = WX_IDX_NONE;
+  }
+};
+
+// Merge the lanes' lists of one wave; lane 0 ends with the wave's K best in
+// out_k/out_i (all lanes compute them).
+__device__ __forceinline__ void wave_merge(TopList &L, wx_u32 (&out_k)[WX_TOPK_K], wx_i64 (&out_i)[WX_TOPK_K]) {
+#pragma unroll 1
+  for (int r = 0; r < WX_TOPK_K; ++r) {
+    wx_u32 bk = L.k[0];
+    wx_i64 bi = L.i[0];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const wx_u32 ok = __shfl_xor(bk, o);
+      const wx_i64 oi = __shfl_xor(bi, o);
+      if (better(ok, oi, bk, bi)) { bk = ok; bi = oi; }
+    }
+    out_k[r] = bk;
+    out_i[r] = bi;
+    if (L.i[0] == bi && L.k[0] == bk && bi != WX_IDX_NONE) L.pop();
+  }
+}
+
+// Merge the wave lists of a block through LDS; every thread of wave 0 returns
+// the block's K best (valid in lane 0).
+__device__ __forceinline__ void block_merge(TopList &L, wx_u32 (*s_k)[WX_TOPK_K], wx_i64 (*s_i)[WX_TOPK_K],
+                                            wx_u32 (&bk)[WX_TOPK_K], wx_i64 (&bi)[WX_TOPK_K]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  wx_u32 wk[WX_TOPK_K];
+  wx_i64 wi[WX_TOPK_K];
+  wave_merge(L, wk, wi);
+  if (lane == 0) {
+#pragma unroll
+    for (int j = 0; j < WX_TOPK_K; ++j) { s_k[wave][j] = wk[j]; s_i[wave][j] = wi[j]; }
+  }
+  __syncthreads();
+  if (wave == 0) {
+    int head[WX_WAVES];
+#pragma unroll
+    for (int w = 0; w < WX_WAVES; ++w) head[w] = 0;
+    for (int r = 0; r < WX_TOPK_K; ++r) {
+      int best = 0;
+      for (int w = 1; w < WX_WAVES; ++w)
+        if (better(s_k[w][head[w]], s_i[w][head[w]], s_k[best][head[best]], s_i[best][head[best]])) best = w;
+      bk[r] = s_k[best][head[best]];
+      bi[r] = s_i[best][head[best]];
+      if (head[best] < WX_TOPK_K - 1) ++head[best];
+      else { s_k[best][head[best]] = 0u; s_i[best][head[best]] = WX_IDX_NONE; }
+    }
+  }
+}
+}  // namespace wx
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs wx_a) {
+  __shared__ wx_u32 s_k[WX_WAVES][WX_TOPK_K];
+  __shared__ wx_i64 s_i[WX_WAVES][WX_TOPK_K];
+  wx::TopList wx_L;
+  wx_L.init();
+  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
+  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq; wx_q0 += wx_stride * WX_UNROLL) {
+#pragma unroll
+    for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+      const wx_i64 wx_q = wx_q0 + wx_u * wx_stride;
+      if (wx_q < wx_nq) {
+        const wx_i64 wx_r0 = wx_q << 2;
+        WX_COLS(WX_DECL_LOAD)
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e) {
+          WX_COLS(WX_BIND_REG)
+          const wx_i64 idx = wx_r0 + wx_e;
+          if (idx < wx_a.n_rows && WX_EVAL_COND()) wx_L.push(wx::rank_of(static_cast<float>(WX_EXPR)), idx);
+        }
+      }
+    }
+  }
+  wx_u32 bk[WX_TOPK_K];
+  wx_i64 bi[WX_TOPK_K];
+  wx::block_merge(wx_L, s_k, s_i, bk, bi);
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int j = 0; j < WX_TOPK_K; ++j) {
+      wx_a.cand_k[(wx_i64)blockIdx.x * WX_TOPK_K + j] = bk[j];
+      wx_a.cand_i[(wx_i64)blockIdx.x * WX_TOPK_K + j] = bi[j];
+    }
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_finalize(WxTopkFinArgs wx_a) {
+  __shared__ wx_u32 s_k[WX_WAVES][WX_TOPK_K];
+  __shared__ wx_i64 s_i[WX_WAVES][WX_TOPK_K];
+  __shared__ wx_u32 s_bk[WX_TOPK_K];
+  __shared__ wx_i64 s_bi[WX_TOPK_K];
+  wx::TopList L;
+  L.init();
+  for (wx_i64 c = threadIdx.x; c < wx_a.n_cand; c += WX_BLOCK)
+    if (wx_a.cand_i[c] != WX_IDX_NONE) L.push(wx_a.cand_k[c], wx_a.cand_i[c]);
+  wx_u32 bk[WX_TOPK_K];
+  wx_i64 bi[WX_TOPK_K];
+  wx::block_merge(L, s_k, s_i, bk, bi);
+  if (threadIdx.x == 0) {
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < WX_TOPK_K; ++j) {
+      s_bk[j] = bk[j];
+      s_bi[j] = bi[j];
+      n += bi[j] != WX_IDX_NONE ? 1 : 0;
+    }
+    if (wx_a.count_out) *wx_a.count_out = n;
+  }
+  __syncthreads();
+  const int wx_j = threadIdx.x;
+  if (wx_j < WX_TOPK_K && s_bi[wx_j] != WX_IDX_NONE) {
+    const wx_i64 idx = s_bi[wx_j];
+    const float wx_key = wx::key_of(s_bk[wx_j]);
+    if (wx_a.out_keys) wx_a.out_keys[wx_j] = wx_key;
+    if (wx_a.out_idx) wx_a.out_idx[wx_j] = wx_a.row_base + idx;
+    if (wx_a.out_vals) {
+#if WX_HAS_SELECT
+      WX_COLS(WX_BIND_PTR)
+      wx_a.out_vals[wx_j] = static_cast<float>(WX_SELECT);
+#else
+      wx_a.out_vals[wx_j] = wx_key;
+#endif
+    }
+  }
+}
+#endif
+
+// ===========================================================================
+#if WX_OP == WX_OP_UTIL
+// Synthetic data generator and the stable sort used by the legacy
+// jit_sort_* entry points (bitonic network over 64-bit (rank << 32 | pos)
+// keys: LDS passes for spans <= 2 * WX_BLOCK * 4, global passes above).
+__device__ __forceinline__ wx_u64 wx_splitmix64(wx_u64 x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_fill_synthetic(WxFillArgs a) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  const float flo = (float)a.lo, fspan = (float)a.hi - (float)a.lo;
+  const wx_i64 ilo = (wx_i64)a.lo, ispan = (wx_i64)a.hi - (wx_i64)a.lo + 1;
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.n; i += stride) {
+    const wx_u64 h = wx_splitmix64((wx_u64)(a.row_base + i) + a.seed * 0xD1B54A32D192ED03ull);
+    double v;
+    if (a.kind == 0) {
+      const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+      const float m = __fmul_rn(u, fspan);
+      v = (double)__fadd_rn(flo, m);
+    } else {
+      v = (double)(ilo + (wx_i64)((h >> 32) % (wx_u64)ispan));
+    }
+    switch (a.dtype) {
+      case 0: static_cast<int *>(a.out)[i] = (int)v; break;
+      case 1: static_cast<wx_i64 *>(a.out)[i] = (wx_i64)v; break;
+      case 2: static_cast<float *>(a.out)[i] = (float)v; break;
+      default: static_cast<double *>(a.out)[i] = v; break;
+    }
+  }
+}
+
+// kind 0: float values, kind 1: int keys.  Descending order inverts the rank
+// but not the position, so equal keys keep their input order (stable).
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_prep(WxSortPrepArgs a) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.npad; i += stride) {
+    wx_u64 e = ~0ull;
+    if (i < a.n) {
+      wx_u32 r;
+      if (a.kind == 0) {
+        const float f = static_cast<const float *>(a.src)[i];
+        r = wx::f2ord(f);
+        if (r == 0u) r = 0xffffffffu;    // NaN sorts last either way
+        else if (!a.ascending) r = ~r;   // 0x007fffff..0x7ffffffe
+      } else {
+        r = (wx_u32)static_cast<const int *>(a.src)[i] ^ 0x80000000u;
+        if (!a.ascending) r = ~r;
+      }
+      e = ((wx_u64)r << 32) | (wx_u32)i;
+    }
+    a.keys[i] = e;
+  }
+}
+
+// LDS bitonic steps on one WX_SORT_LDS-element slice per block: for every
+// stage k in [a.k, a.j] (a.j = kend) run all partner distances below
+// WX_SORT_LDS.  The first launch covers k = 2 .. WX_SORT_LDS; afterwards each
+// larger stage runs its long distances globally and finishes here.
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_bitonic_lds(WxSortPassArgs a) {
+  __shared__ wx_u64 s[WX_SORT_LDS];
+  const wx_i64 base = (wx_i64)blockIdx.x * WX_SORT_LDS;
+  for (int i = threadIdx.x; i < WX_SORT_LDS; i += WX_BLOCK) s[i] = a.keys[base + i];
+  __syncthreads();
+  for (wx_i64 k = a.k; k <= a.j; k <<= 1) {
+    wx_i64 j = k >> 1;
+    if (j >= WX_SORT_LDS) j = WX_SORT_LDS >> 1;
+    for (; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < WX_SORT_LDS; i += WX_BLOCK) {
+        const int p = i ^ (int)j;
+        if (p > i) {
+          const wx_u64 x = s[i], y = s[p];
+          const bool up = ((base + i) & k) == 0;
+          if ((x > y) == up) { s[i] = y; s[p] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < WX_SORT_LDS; i += WX_BLOCK) a.keys[base + i] = s[i];
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_bitonic_global(WxSortPassArgs a) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.npad; i += stride) {
+    const wx_i64 p = i ^ a.j;
+    if (p > i) {
+      const wx_u64 x = a.keys[i], y = a.keys[p];
+      const bool up = (i & a.k) == 0;
+      if ((x > y) == up) { a.keys[i] = y; a.keys[p] = x; }
+    }
+  }
+}
+
+// Apply the permutation: dst[r] = src[pos(keys[r])] for 4-byte payloads
+// (float values, or int keys plus float values).
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApplyArgs a) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 r = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; r < a.n; r += stride) {
+    const wx_u32 p = (wx_u32)a.keys[r];
+    static_cast<wx_u32 *>(a.dst_a)[r] = static_cast<const wx_u32 *>(a.src_a)[p];
+    if (a.src_v) a.dst_v[r] = a.src_v[p];
+  }
+}
+#endif
