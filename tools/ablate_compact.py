@@ -1,0 +1,108 @@
+#!/usr/bin/env python3
+"""A/B the compaction kernel variants in one process (GPU).  Diagnostic only.
+
+Each variant is selected through the environment knobs read per call by
+libwarpexec (WARPDB_COMPACT_GROUPS / _SCHED / _BPC, WARPDB_EXTRA_DEFINES);
+timings are HIP events around the kernel (WX_F_TIME), interleaved rounds.
+"""
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import torch  # noqa: E402
+
+from warpdb_amd import _warpexec as wx  # noqa: E402
+
+n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 1_000_000_000
+rounds = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+torch.cuda.set_device(0)
+stream = torch.cuda.current_stream().cuda_stream
+L = wx.make_launch(stream=stream, flags=0)
+Lt = wx.make_launch(stream=stream, flags=wx.F_TIME)
+price = torch.empty(n, dtype=torch.float32, device="cuda")
+qty = torch.empty(n, dtype=torch.float32, device="cuda")
+wx.fill_synthetic(price.data_ptr(), wx.FLOAT32, n, 1, 0, 0.0, 40.0, L)
+wx.fill_synthetic(qty.data_ptr(), wx.FLOAT32, n, 2, 1, 1, 100, L)
+table = wx.Table(n, [wx.Column("price", wx.FLOAT32, price.data_ptr()), wx.Column("quantity", wx.FLOAT32, qty.data_ptr())])
+out_v = torch.empty(n, dtype=torch.float32, device="cuda")
+out_i = torch.empty(n, dtype=torch.int32, device="cuda")
+cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+ref_count = int((price > 15.0).sum().item())
+
+VARIANTS = {
+    "static_g4": {},
+    "ticket_g4": {"WARPDB_COMPACT_SCHED": "ticket"},
+    "static_g4_nopf": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_PREFETCH=0"},
+    "static_g4_lb1": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=1"},
+    "static_g4_lb8": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=8"},
+    "static_g2": {"WARPDB_COMPACT_GROUPS": "2"},
+    "static_g8": {"WARPDB_COMPACT_GROUPS": "8"},
+    "static_g4_bpc2": {"WARPDB_COMPACT_BPC": "2"},
+    "static_g4_force4": {"WARPDB_COMPACT_BPC_FORCE": "4"},
+    "static_g4_nopf_force5": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_PREFETCH=0", "WARPDB_COMPACT_BPC_FORCE": "5"},
+    "static_g4_nolookback": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK"},
+    "static_g4_nostore": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_STORE"},
+}
+if len(sys.argv) > 3:
+    VARIANTS = {k: v for k, v in VARIANTS.items() if k in sys.argv[3].split(",")}
+KNOBS = ("WARPDB_COMPACT_SCHED", "WARPDB_COMPACT_GROUPS", "WARPDB_COMPACT_BPC", "WARPDB_EXTRA_DEFINES",
+         "WARPDB_COMPACT_BPC_FORCE")
+
+
+def setenv(v):
+    for k in KNOBS:
+        os.environ.pop(k, None)
+    os.environ.update(v)
+
+
+def run(Lx):
+    wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", Lx, wx.MODE_COMPACT,
+                      out_v.data_ptr(), out_i.data_ptr(), 4, 0, d_count=cnt.data_ptr())
+
+
+res = {k: [] for k in VARIANTS}
+for name, v in VARIANTS.items():  # compile + warm
+    setenv(v)
+    t0 = time.time()
+    run(L)
+    run(L)
+    wx.check(L)
+    ok = "diag" if "DIAG" in str(v) else ("ok" if int(cnt.item()) == ref_count else f"BAD {int(cnt.item())} vs {ref_count}")
+    print(f"{name:24s} warm {time.time() - t0:5.2f}s  count {ok}", flush=True)
+wx.timing_read()
+for r in range(rounds):
+    for name, v in VARIANTS.items():
+        setenv(v)
+        run(Lt)
+        ms, k = wx.timing_read()
+        res[name].append(ms / k)
+bytes_ = n * 8 + ref_count * 8
+for name, ts in res.items():
+    ts.sort()
+    med = ts[len(ts) // 2]
+    print(f"{name:24s} median {med:8.3f} ms  min {ts[0]:8.3f}  {bytes_ / med / 1e6:8.1f} GB/s  {n / med / 1e6:8.2f} Grows/s")
+
+# references: read-only SUM over both columns, torch copy
+setenv({})
+wx.reduce_sum(table, "(price[idx] * quantity[idx])", None, L)
+ts = []
+for _ in range(rounds):
+    wx.reduce_sum(table, "(price[idx] * quantity[idx])", None, Lt, want_host=False)
+    ms, k = wx.timing_read()
+    ts.append(ms / k)
+ts.sort()
+print(f"{'sum_read_8B':24s} median {ts[len(ts)//2]:8.3f} ms  {n * 8 / ts[len(ts)//2] / 1e6:8.1f} GB/s (read)")
+e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+tmp = torch.empty_like(price)
+tmp.copy_(price)
+ts = []
+for _ in range(rounds):
+    e0.record()
+    tmp.copy_(price)
+    e1.record()
+    e1.synchronize()
+    ts.append(e0.elapsed_time(e1))
+ts.sort()
+print(f"{'torch_copy_4B':24s} median {ts[len(ts)//2]:8.3f} ms  {n * 8 / ts[len(ts)//2] / 1e6:8.1f} GB/s (r+w)")

@@ -25,7 +25,9 @@ typedef unsigned int wx_u32;
 #define WX_OP_TOPK 4
 #define WX_OP_UTIL 5
 
-#define WX_COMPACT_GROUPS 4
+#ifndef WX_COMPACT_GROUPS
+#define WX_COMPACT_GROUPS 4  // row quads per thread per tile (host passes its choice)
+#endif
 #define WX_COMPACT_TILE (WX_BLOCK * 4 * WX_COMPACT_GROUPS)
 #define WX_GROUP_WINDOW 2048
 #define WX_GROUP_HSORT_MAX 4096

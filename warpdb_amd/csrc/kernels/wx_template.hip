@@ -18,6 +18,10 @@
 // loads per lane (one 1 KiB access per wave-instruction), everything else
 // kept in registers / LDS.  MFMA is not used: nothing here is a contraction.
 
+#if !defined(__HIPCC_RTC__)
+#include <hip/hip_runtime.h>  // offline hipcc builds; hiprtc provides these itself
+#endif
+
 #ifndef WX_ALIGNED16
 #define WX_ALIGNED16 0
 #endif
@@ -177,125 +181,211 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 #define WX_SPIN_LIMIT (1u << 24)
 #endif
 
+// Schedule: WX_COMPACT_STATIC (default) runs a persistent grid no larger
+// than what is co-resident; block b takes tiles b, b + grid, ... in order, so
+// the predecessors of every tile belong to running blocks.  Otherwise each
+// block takes one tile from a ticket counter (robust to any residency, but a
+// single counter word serialises at ~88 tickets/us on MI355X).
+#ifndef WX_COMPACT_STATIC
+#define WX_COMPACT_STATIC 1
+#endif
+
+#ifndef WX_COMPACT_PREFETCH
+#define WX_COMPACT_PREFETCH 1  // issue tile t+grid's loads before tile t's look-back
+#endif
+#ifndef WX_LB_PER_LANE
+#define WX_LB_PER_LANE 4       // predecessors inspected per lane per look-back round
+#endif
+
+// Per-column input registers of one tile and the load/bind helpers.
+#define WX_DECL_TILE_IN(name, T, slot) T wx_in##slot[WX_GROUPS][4];
+#define WX_LOAD_TILE_IN(name, T, slot) \
+  ::wx::load4<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)threadIdx.x * 4, wx_a.n_rows, wx_in##slot[wx_g]);
+#define WX_BIND_TILE_IN(name, T, slot) const ::wx::reg<T> name{wx_in##slot[wx_g][wx_e]};
+
+// Exclusive prefix of `tile` from its predecessors' status words; run by one
+// wave.  Each lane inspects WX_LB_PER_LANE consecutive predecessors, so one
+// round covers 64 * WX_LB_PER_LANE tiles.
+__device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 tile) {
+  const int lane = threadIdx.x & 63;
+  wx_i64 excl = 0;
+  wx_i64 look = tile - 1;
+  wx_u32 spins = 0;
+  while (true) {
+    wx_u64 st[WX_LB_PER_LANE];
+#pragma unroll
+    for (int j = 0; j < WX_LB_PER_LANE; ++j) {
+      const wx_i64 t = look - (wx_i64)lane * WX_LB_PER_LANE - j;
+      st[j] = t >= 0 ? wx::ld_agent(&a.status[t]) : WX_FLAG_P;  // "tile -1": inclusive 0
+    }
+#pragma unroll
+    for (int j = 0; j < WX_LB_PER_LANE; ++j) {
+      const wx_i64 t = look - (wx_i64)lane * WX_LB_PER_LANE - j;
+      while ((st[j] >> 62) == 0ull) {
+        __builtin_amdgcn_s_sleep(1);
+        st[j] = wx::ld_agent(&a.status[t]);
+        if (++spins > WX_SPIN_LIMIT) {
+          atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_LOOKBACK);
+          st[j] = WX_FLAG_P;
+        }
+      }
+    }
+    // nearest inclusive prefix in this lane (distance order j = 0, 1, ...)
+    int firstp = WX_LB_PER_LANE;
+    wx_u64 all = 0;
+#pragma unroll
+    for (int j = WX_LB_PER_LANE - 1; j >= 0; --j) {
+      all += st[j] & WX_VAL_MASK;
+      if ((st[j] >> 62) == 2ull) firstp = j;
+    }
+    wx_u64 part = 0;
+#pragma unroll
+    for (int j = 0; j < WX_LB_PER_LANE; ++j) part += (j <= firstp) ? (st[j] & WX_VAL_MASK) : 0ull;
+    const wx_u64 pmask = __builtin_amdgcn_ballot_w64(firstp < WX_LB_PER_LANE);
+    if (pmask) {
+      const int fl = __builtin_ctzll(pmask);
+      const wx_u64 mine = lane < fl ? all : (lane == fl ? part : 0ull);
+      excl += (wx_i64)wx::wave_sum_u64(mine);
+      break;
+    }
+    excl += (wx_i64)wx::wave_sum_u64(all);
+    look -= 64 * WX_LB_PER_LANE;
+  }
+  return excl;
+}
+
 extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_compact(WxCompactArgs wx_a) {
   __shared__ wx_u32 s_wave_cnt[WX_WAVES][WX_GROUPS];
   __shared__ wx_i64 s_excl;
-  __shared__ wx_u32 s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
+#if WX_COMPACT_STATIC
+  wx_i64 tile = blockIdx.x;
+  const wx_i64 tile_step = gridDim.x;
+#else
+  __shared__ wx_u32 s_tile;
   if (tid == 0)
     s_tile = (wx_u32)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
-  const wx_i64 tile = s_tile;
-  const wx_i64 tile_base = tile * WX_TILE;
-
-  bool wx_keep[WX_GROUPS][4];
-  float wx_val[WX_GROUPS][4];
+  wx_i64 tile = s_tile;
+  const wx_i64 tile_step = wx_a.n_tiles;  // one tile per block
+#endif
+  WX_COLS(WX_DECL_TILE_IN)
+  if (tile < wx_a.n_tiles) {
+    const wx_i64 wx_tb = tile * WX_TILE;
 #pragma unroll
-  for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
-    const wx_i64 wx_r0 = tile_base + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)tid * 4;
-    WX_COLS(WX_DECL_LOAD)
-#pragma unroll
-    for (int wx_e = 0; wx_e < 4; ++wx_e) {
-      WX_COLS(WX_BIND_REG)
-      const wx_i64 idx = wx_r0 + wx_e;
-      bool wx_k = idx < wx_a.n_rows;
-      wx_k = wx_k && WX_EVAL_COND();
-      wx_keep[wx_g][wx_e] = wx_k;
-      wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
-    }
+    for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
   }
-
-  // In-tile ranks: per (group, e) one 64-bit ballot.
-  wx_u32 lane_pre[WX_GROUPS];
+  while (tile < wx_a.n_tiles) {
+    const wx_i64 tile_base = tile * WX_TILE;
+    bool wx_keep[WX_GROUPS][4];
+    float wx_val[WX_GROUPS][4];
 #pragma unroll
-  for (int g = 0; g < WX_GROUPS; ++g) {
-    wx_u32 pre = 0, tot = 0;
+    for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const wx_u64 m = __builtin_amdgcn_ballot_w64(wx_keep[g][e]);
-      pre += wx::lanes_below(m);
-      tot += (wx_u32)__builtin_popcountll(m);
+      for (int wx_e = 0; wx_e < 4; ++wx_e) {
+        WX_COLS(WX_BIND_TILE_IN)
+        const wx_i64 idx = tile_base + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)threadIdx.x * 4 + wx_e;
+        bool wx_k = idx < wx_a.n_rows;
+        wx_k = wx_k && WX_EVAL_COND();
+        wx_keep[wx_g][wx_e] = wx_k;
+        wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
+      }
     }
-    lane_pre[g] = pre;
-    if (lane == 0) s_wave_cnt[wave][g] = tot;
-  }
-  __syncthreads();
 
-  wx_u32 grp_base[WX_GROUPS];
-  wx_u32 block_total = 0;
+    // In-tile ranks: per (group, e) one 64-bit ballot.
+    wx_u32 lane_pre[WX_GROUPS];
 #pragma unroll
-  for (int g = 0; g < WX_GROUPS; ++g) {
-    wx_u32 before = 0, gsum = 0;
+    for (int g = 0; g < WX_GROUPS; ++g) {
+      wx_u32 pre = 0, tot = 0;
 #pragma unroll
-    for (int w = 0; w < WX_WAVES; ++w) {
-      const wx_u32 c = s_wave_cnt[w][g];
-      before += (w < wave) ? c : 0u;
-      gsum += c;
+      for (int e = 0; e < 4; ++e) {
+        const wx_u64 m = __builtin_amdgcn_ballot_w64(wx_keep[g][e]);
+        pre += wx::lanes_below(m);
+        tot += (wx_u32)__builtin_popcountll(m);
+      }
+      lane_pre[g] = pre;
+      if (lane == 0) s_wave_cnt[wave][g] = tot;
     }
-    grp_base[g] = block_total + before;
-    block_total += gsum;
-  }
+    __syncthreads();
 
-  // Decoupled look-back (wave 0).
-  if (wave == 0) {
-    wx_i64 excl = 0;
-    if (tile == 0) {
-      if (lane == 0) wx::st_agent(&wx_a.status[0], WX_FLAG_P | (wx_u64)block_total);
-    } else {
-      if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_A | (wx_u64)block_total);
-      wx_i64 look = tile - 1;
-      wx_u32 spins = 0;
-      while (true) {
-        const wx_i64 t = look - lane;
-        wx_u64 s = WX_FLAG_P;  // "tile -1": inclusive prefix 0
-        if (t >= 0) {
-          s = wx::ld_agent(&wx_a.status[t]);
-          while ((s >> 62) == 0ull) {
-            __builtin_amdgcn_s_sleep(1);
-            s = wx::ld_agent(&wx_a.status[t]);
-            if (++spins > WX_SPIN_LIMIT) {
-              atomicOr(reinterpret_cast<unsigned int *>(&wx_a.ctrs[1]), WX_DEVERR_LOOKBACK);
-              s = WX_FLAG_P;
-            }
+    const wx_i64 next = tile + tile_step;
+#if WX_COMPACT_PREFETCH
+    if (next < wx_a.n_tiles) {
+      const wx_i64 wx_tb = next * WX_TILE;
+#pragma unroll
+      for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
+    }
+#endif
+
+    wx_u32 grp_base[WX_GROUPS];
+    wx_u32 block_total = 0;
+#pragma unroll
+    for (int g = 0; g < WX_GROUPS; ++g) {
+      wx_u32 before = 0, gsum = 0;
+#pragma unroll
+      for (int w = 0; w < WX_WAVES; ++w) {
+        const wx_u32 c = s_wave_cnt[w][g];
+        before += (w < wave) ? c : 0u;
+        gsum += c;
+      }
+      grp_base[g] = block_total + before;
+      block_total += gsum;
+    }
+
+    if (wave == 0) {
+      wx_i64 excl = 0;
+#if WX_DIAG_NO_LOOKBACK
+      excl = tile_base / 2;  // diagnostic build: timing only, results invalid
+#else
+      if (tile == 0) {
+        if (lane == 0) wx::st_agent(&wx_a.status[0], WX_FLAG_P | (wx_u64)block_total);
+      } else {
+        if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_A | (wx_u64)block_total);
+        excl = wx_lookback(wx_a, tile);
+        if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_P | (wx_u64)(excl + block_total));
+      }
+#endif
+      if (lane == 0) s_excl = excl;
+    }
+    __syncthreads();
+    const wx_i64 excl = s_excl;
+
+#if WX_DIAG_NO_STORE
+    float sink = 0.0f;
+#pragma unroll
+    for (int g = 0; g < WX_GROUPS; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) sink += wx_keep[g][e] ? wx_val[g][e] + (float)(excl + grp_base[g] + lane_pre[g]) : 0.0f;
+    if (sink == -1.0f && wx_a.out_val) wx_a.out_val[0] = sink;  // keeps the work alive
+#else
+#pragma unroll
+    for (int g = 0; g < WX_GROUPS; ++g) {
+      const wx_i64 r0 = tile_base + (wx_i64)g * (WX_BLOCK * 4) + (wx_i64)tid * 4;
+      wx_i64 pos = excl + grp_base[g] + lane_pre[g];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if (wx_keep[g][e]) {
+          if (wx_a.out_val) wx_a.out_val[pos] = wx_val[g][e];
+          if (wx_a.out_idx) {
+            const wx_i64 gi = wx_a.row_base + r0 + e;
+            if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
+            else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
           }
+          ++pos;
         }
-        const wx_u64 pmask = __builtin_amdgcn_ballot_w64((s >> 62) == 2ull);
-        wx_u64 v = s & WX_VAL_MASK;
-        if (pmask) {
-          const int first = __builtin_ctzll(pmask);
-          v = (lane <= first) ? v : 0ull;
-          excl += (wx_i64)wx::wave_sum_u64(v);
-          break;
-        }
-        excl += (wx_i64)wx::wave_sum_u64(v);
-        look -= 64;
-      }
-      if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_P | (wx_u64)(excl + block_total));
-    }
-    if (lane == 0) s_excl = excl;
-  }
-  __syncthreads();
-  const wx_i64 excl = s_excl;
-
-#pragma unroll
-  for (int g = 0; g < WX_GROUPS; ++g) {
-    const wx_i64 r0 = tile_base + (wx_i64)g * (WX_BLOCK * 4) + (wx_i64)tid * 4;
-    wx_i64 pos = excl + grp_base[g] + lane_pre[g];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      if (wx_keep[g][e]) {
-        if (wx_a.out_val) wx_a.out_val[pos] = wx_val[g][e];
-        if (wx_a.out_idx) {
-          const wx_i64 gi = wx_a.row_base + r0 + e;
-          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
-          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
-        }
-        ++pos;
       }
     }
+#endif
+    if (tid == 0 && tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
+#if !WX_COMPACT_PREFETCH
+    if (next < wx_a.n_tiles) {
+      const wx_i64 wx_tb = next * WX_TILE;
+#pragma unroll
+      for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
+    }
+#endif
+    tile = next;
   }
-  if (tid == 0 && tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
 }
 #endif
 
