@@ -32,18 +32,14 @@ cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
 ref_count = int((price > 15.0).sum().item())
 
 VARIANTS = {
-    "static_g4": {},
-    "ticket_g4": {"WARPDB_COMPACT_SCHED": "ticket"},
-    "static_g4_nopf": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_PREFETCH=0"},
-    "static_g4_lb1": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=1"},
-    "static_g4_lb8": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=8"},
-    "static_g2": {"WARPDB_COMPACT_GROUPS": "2"},
-    "static_g8": {"WARPDB_COMPACT_GROUPS": "8"},
-    "static_g4_bpc2": {"WARPDB_COMPACT_BPC": "2"},
-    "static_g4_force4": {"WARPDB_COMPACT_BPC_FORCE": "4"},
-    "static_g4_nopf_force5": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_PREFETCH=0", "WARPDB_COMPACT_BPC_FORCE": "5"},
-    "static_g4_nolookback": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK"},
-    "static_g4_nostore": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_STORE"},
+    "pipe_g4_lb2": {},
+    "pipe_g4_lb1": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=1"},
+    "pipe_g4_lb4": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=4"},
+    "pipe_g4_lb8": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=8"},
+    "pipe_g4_lb2_sl0": {"WARPDB_EXTRA_DEFINES": "WX_LB_SLEEP=0"},
+    "pipe_g4_lb2_sl8": {"WARPDB_EXTRA_DEFINES": "WX_LB_SLEEP=8"},
+    "ticket_g4_lb2": {"WARPDB_COMPACT_SCHED": "ticket"},
+    "pipe_g4_nolookback": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK"},
 }
 if len(sys.argv) > 3:
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in sys.argv[3].split(",")}

@@ -33,6 +33,7 @@ typedef unsigned int wx_u32;
 #define WX_GROUP_HSORT_MAX 4096
 #define WX_TOPK_MAX 32
 #define WX_SORT_LDS (WX_BLOCK * 8)
+#define WX_COMPACT_CBLOCK (WX_BLOCK + 64)  // 4 data waves + 1 control wave
 
 struct WxDenseArgs {
   const void *col[WX_MAX_COLS];
@@ -45,7 +46,7 @@ struct WxCompactArgs {
   const void *col[WX_MAX_COLS];
   float *out_val;     // nullable
   void *out_idx;      // nullable; int32 or int64
-  wx_u64 *status;     // [n_tiles], zeroed per call
+  wx_u64 *status;     // [n_tiles + 1], zeroed per call; [n_tiles] = abort word
   wx_u64 *ctrs;       // [0] tile ticket (zeroed per call), [1] error bits
   wx_i64 *count_out;  // nullable
   wx_i64 n_rows;

@@ -161,51 +161,54 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 
 // ===========================================================================
 #if WX_OP == WX_OP_COMPACT
-// Ordered stream compaction, single pass with decoupled look-back.
+// Ordered stream compaction in one pass: decoupled look-back over tiles.
 //
-// Tile = 256 threads x WX_GROUPS groups x 4 rows.  Row (g, thread, e) of a
-// tile sits at offset g*1024 + thread*4 + e, so every group is one 16-byte
-// load per lane per column.  In-tile ranks come from wavefront ballots
-// (v_mbcnt) and a 4-wave x WX_GROUPS LDS table; the tile's global offset from
-// the predecessors' 8-byte status words {flag:2 | value:62}.  A status word
-// is its own payload (written and read by single agent-scope 8-byte atomics),
-// so no fence is needed; output rows are never read inside the launch.
-// Tiles are taken in order from a ticket counter, so every predecessor of a
-// tile is already resident: the look-back always terminates.
+// Tile = 256 data threads x WX_GROUPS groups x 4 rows; row (g, thread, e)
+// of a tile is at offset g*1024 + thread*4 + e, so each group is one 16-byte
+// load per lane per column.  In-tile ranks come from 64-bit wavefront ballots
+// (v_mbcnt) and a 4-wave x WX_GROUPS LDS table.  A tile's global offset comes
+// from its predecessors' 8-byte status words {flag:2 | value:62}; a status
+// word is its own payload (single agent-scope 8-byte stores and loads), so no
+// fence is needed, and output rows are never read inside the launch.
+//
+// wx_project_compact (default) is a persistent, software-pipelined kernel:
+// 4 data waves + 1 control wave per workgroup.  Iteration k: the data waves
+// evaluate tile t_k (its loads were issued one iteration earlier), rank the
+// passing rows, stage (value, tile-local row) in LDS and issue the loads of
+// t_{k+1}; the control wave publishes t_k's aggregate and runs its look-back
+// while the data waves store t_{k-1} from LDS (coalesced) and evaluate
+// t_{k+1}.  Block b owns tiles b, b + grid, ... so the grid must be
+// co-resident (the host sizes it from the occupancy query).
+// wx_project_compact_ticket takes one tile per workgroup from a ticket
+// counter: no residency assumption, no pipelining.
 #define WX_GROUPS WX_COMPACT_GROUPS
 #define WX_TILE WX_COMPACT_TILE
+#define WX_CBLOCK (WX_BLOCK + 64)
 #define WX_FLAG_A (1ull << 62)
 #define WX_FLAG_P (2ull << 62)
 #define WX_VAL_MASK ((1ull << 62) - 1ull)
 #ifndef WX_SPIN_LIMIT
-#define WX_SPIN_LIMIT (1u << 24)
-#endif
-
-// Schedule: WX_COMPACT_STATIC (default) runs a persistent grid no larger
-// than what is co-resident; block b takes tiles b, b + grid, ... in order, so
-// the predecessors of every tile belong to running blocks.  Otherwise each
-// block takes one tile from a ticket counter (robust to any residency, but a
-// single counter word serialises at ~88 tickets/us on MI355X).
-#ifndef WX_COMPACT_STATIC
-#define WX_COMPACT_STATIC 1
-#endif
-
-#ifndef WX_COMPACT_PREFETCH
-#define WX_COMPACT_PREFETCH 1  // issue tile t+grid's loads before tile t's look-back
+#define WX_SPIN_LIMIT (1u << 20)
 #endif
 #ifndef WX_LB_PER_LANE
-#define WX_LB_PER_LANE 4       // predecessors inspected per lane per look-back round
+#define WX_LB_PER_LANE 1  // predecessors per lane per look-back round (1 measured fastest: each agent-scope poll is costly)
+#endif
+#ifndef WX_LB_SLEEP
+#define WX_LB_SLEEP 2     // s_sleep units (64 clocks) between polls of an unpublished tile
 #endif
 
 // Per-column input registers of one tile and the load/bind helpers.
 #define WX_DECL_TILE_IN(name, T, slot) T wx_in##slot[WX_GROUPS][4];
 #define WX_LOAD_TILE_IN(name, T, slot) \
-  ::wx::load4<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)threadIdx.x * 4, wx_a.n_rows, wx_in##slot[wx_g]);
+  ::wx::load4<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)wx_dt * 4, wx_a.n_rows, wx_in##slot[wx_g]);
 #define WX_BIND_TILE_IN(name, T, slot) const ::wx::reg<T> name{wx_in##slot[wx_g][wx_e]};
 
-// Exclusive prefix of `tile` from its predecessors' status words; run by one
-// wave.  Each lane inspects WX_LB_PER_LANE consecutive predecessors, so one
-// round covers 64 * WX_LB_PER_LANE tiles.
+// Exclusive prefix of `tile` from its predecessors' status words; one wave.
+// Load j of lane l reads tile look - 64*j - l: every load instruction covers
+// 64 adjacent status words (agent-scope loads are served beyond L2, so poll
+// traffic competes with the table stream).  A timed-out wait raises the error
+// bit, and every waiter that sees the bit gives up, so a broken residency
+// assumption drains the grid quickly instead of hanging it.
 __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 tile) {
   const int lane = threadIdx.x & 63;
   wx_i64 excl = 0;
@@ -215,177 +218,243 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
     wx_u64 st[WX_LB_PER_LANE];
 #pragma unroll
     for (int j = 0; j < WX_LB_PER_LANE; ++j) {
-      const wx_i64 t = look - (wx_i64)lane * WX_LB_PER_LANE - j;
+      const wx_i64 t = look - 64 * j - lane;
       st[j] = t >= 0 ? wx::ld_agent(&a.status[t]) : WX_FLAG_P;  // "tile -1": inclusive 0
     }
+    // Wait only for the entries nearer than the nearest inclusive prefix
+    // already visible (distance order (j, lane)); farther ones do not matter.
+    int near_p = 64 * WX_LB_PER_LANE;  // distance of the nearest P, or window size
+    while (true) {
+      near_p = 64 * WX_LB_PER_LANE;
+      bool pending = false;
 #pragma unroll
-    for (int j = 0; j < WX_LB_PER_LANE; ++j) {
-      const wx_i64 t = look - (wx_i64)lane * WX_LB_PER_LANE - j;
-      while ((st[j] >> 62) == 0ull) {
-        __builtin_amdgcn_s_sleep(1);
-        st[j] = wx::ld_agent(&a.status[t]);
-        if (++spins > WX_SPIN_LIMIT) {
+      for (int j = WX_LB_PER_LANE - 1; j >= 0; --j) {
+        const wx_u64 pm = __builtin_amdgcn_ballot_w64((st[j] >> 62) == 2ull);
+        if (pm) near_p = 64 * j + __builtin_ctzll(pm);
+      }
+#pragma unroll
+      for (int j = 0; j < WX_LB_PER_LANE; ++j) {
+        const bool need = (st[j] >> 62) == 0ull && 64 * j + lane < near_p;
+        pending |= __builtin_amdgcn_ballot_w64(need) != 0ull;
+      }
+      if (!pending) break;
+      __builtin_amdgcn_s_sleep(WX_LB_SLEEP);
+#pragma unroll
+      for (int j = 0; j < WX_LB_PER_LANE; ++j) {
+        if ((st[j] >> 62) == 0ull && 64 * j + lane < near_p) st[j] = wx::ld_agent(&a.status[look - 64 * j - lane]);
+      }
+      if ((++spins & 63u) == 0u) {
+        if (spins > WX_SPIN_LIMIT) {  // sticky error for the host + this launch's abort word
           atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_LOOKBACK);
-          st[j] = WX_FLAG_P;
+          wx::st_agent(&a.status[a.n_tiles], 1ull);
+        }
+        if (wx::ld_agent(&a.status[a.n_tiles])) {
+#pragma unroll
+          for (int j = 0; j < WX_LB_PER_LANE; ++j) st[j] = WX_FLAG_P;
         }
       }
     }
-    // nearest inclusive prefix in this lane (distance order j = 0, 1, ...)
-    int firstp = WX_LB_PER_LANE;
-    wx_u64 all = 0;
+    wx_u64 v = 0;
 #pragma unroll
-    for (int j = WX_LB_PER_LANE - 1; j >= 0; --j) {
-      all += st[j] & WX_VAL_MASK;
-      if ((st[j] >> 62) == 2ull) firstp = j;
-    }
-    wx_u64 part = 0;
-#pragma unroll
-    for (int j = 0; j < WX_LB_PER_LANE; ++j) part += (j <= firstp) ? (st[j] & WX_VAL_MASK) : 0ull;
-    const wx_u64 pmask = __builtin_amdgcn_ballot_w64(firstp < WX_LB_PER_LANE);
-    if (pmask) {
-      const int fl = __builtin_ctzll(pmask);
-      const wx_u64 mine = lane < fl ? all : (lane == fl ? part : 0ull);
-      excl += (wx_i64)wx::wave_sum_u64(mine);
-      break;
-    }
-    excl += (wx_i64)wx::wave_sum_u64(all);
+    for (int j = 0; j < WX_LB_PER_LANE; ++j)
+      if (64 * j + lane <= near_p && 64 * j + lane < 64 * WX_LB_PER_LANE) v += st[j] & WX_VAL_MASK;
+    excl += (wx_i64)wx::wave_sum_u64(v);
+    if (near_p < 64 * WX_LB_PER_LANE) break;
     look -= 64 * WX_LB_PER_LANE;
   }
   return excl;
 }
 
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_compact(WxCompactArgs wx_a) {
-  __shared__ wx_u32 s_wave_cnt[WX_WAVES][WX_GROUPS];
-  __shared__ wx_i64 s_excl;
+// Evaluate one tile held in wx_in* registers and rank its passing rows.
+// Writes per-wave totals to s_cnt and returns per-lane ranks in lane_pre.
+#define WX_EVAL_AND_RANK(S_CNT)                                                                          \
+  _Pragma("unroll") for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {                                     \
+    _Pragma("unroll") for (int wx_e = 0; wx_e < 4; ++wx_e) {                                           \
+      WX_COLS(WX_BIND_TILE_IN)                                                                           \
+      const wx_i64 idx = tile_base + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)wx_dt * 4 + wx_e;          \
+      bool wx_k = idx < wx_a.n_rows;                                                                     \
+      wx_k = wx_k && WX_EVAL_COND();                                                                     \
+      wx_keep[wx_g][wx_e] = wx_k;                                                                        \
+      wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);                                                  \
+    }                                                                                                    \
+  }                                                                                                      \
+  _Pragma("unroll") for (int g = 0; g < WX_GROUPS; ++g) {                                              \
+    wx_u32 pre = 0, tot = 0;                                                                             \
+    _Pragma("unroll") for (int e = 0; e < 4; ++e) {                                                    \
+      const wx_u64 m = __builtin_amdgcn_ballot_w64(wx_keep[g][e]);                                       \
+      pre += wx::lanes_below(m);                                                                         \
+      tot += (wx_u32)__builtin_popcountll(m);                                                            \
+    }                                                                                                    \
+    lane_pre[g] = pre;                                                                                   \
+    if (lane == 0) S_CNT[wave][g] = tot;                                                                 \
+  }
+
+#define WX_BASES(S_CNT)                                        \
+  _Pragma("unroll") for (int g = 0; g < WX_GROUPS; ++g) {    \
+    wx_u32 before = 0, gsum = 0;                               \
+    _Pragma("unroll") for (int w = 0; w < WX_WAVES; ++w) {   \
+      const wx_u32 c = S_CNT[w][g];                            \
+      before += (w < wave) ? c : 0u;                           \
+      gsum += c;                                               \
+    }                                                          \
+    grp_base[g] = block_total + before;                        \
+    block_total += gsum;                                       \
+  }
+
+extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCompactArgs wx_a) {
+  __shared__ wx_u32 s_cnt[2][WX_WAVES][WX_GROUPS];
+  __shared__ float s_val[2][WX_TILE];
+  __shared__ unsigned short s_off[2][WX_TILE];
+  __shared__ wx_i64 s_excl[2];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#if WX_COMPACT_STATIC
+  const bool control = wave == WX_WAVES;
+  const int wx_dt = tid;  // data-thread index (data waves only)
+  const wx_i64 grid = gridDim.x;
   wx_i64 tile = blockIdx.x;
-  const wx_i64 tile_step = gridDim.x;
-#else
-  __shared__ wx_u32 s_tile;
-  if (tid == 0)
-    s_tile = (wx_u32)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  wx_i64 tile = s_tile;
-  const wx_i64 tile_step = wx_a.n_tiles;  // one tile per block
-#endif
   WX_COLS(WX_DECL_TILE_IN)
-  if (tile < wx_a.n_tiles) {
+  if (!control && tile < wx_a.n_tiles) {
     const wx_i64 wx_tb = tile * WX_TILE;
 #pragma unroll
     for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
   }
-  while (tile < wx_a.n_tiles) {
+  wx_u32 prev_total = 0;
+  for (int k = 0;; ++k) {
+    const bool have = tile < wx_a.n_tiles;
+    const bool have_prev = k > 0 && tile - grid < wx_a.n_tiles;
+    if (!have && !have_prev) break;
+    const int buf = k & 1;
     const wx_i64 tile_base = tile * WX_TILE;
     bool wx_keep[WX_GROUPS][4];
     float wx_val[WX_GROUPS][4];
-#pragma unroll
-    for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
-#pragma unroll
-      for (int wx_e = 0; wx_e < 4; ++wx_e) {
-        WX_COLS(WX_BIND_TILE_IN)
-        const wx_i64 idx = tile_base + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)threadIdx.x * 4 + wx_e;
-        bool wx_k = idx < wx_a.n_rows;
-        wx_k = wx_k && WX_EVAL_COND();
-        wx_keep[wx_g][wx_e] = wx_k;
-        wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
-      }
-    }
-
-    // In-tile ranks: per (group, e) one 64-bit ballot.
     wx_u32 lane_pre[WX_GROUPS];
-#pragma unroll
-    for (int g = 0; g < WX_GROUPS; ++g) {
-      wx_u32 pre = 0, tot = 0;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const wx_u64 m = __builtin_amdgcn_ballot_w64(wx_keep[g][e]);
-        pre += wx::lanes_below(m);
-        tot += (wx_u32)__builtin_popcountll(m);
-      }
-      lane_pre[g] = pre;
-      if (lane == 0) s_wave_cnt[wave][g] = tot;
-    }
+    // phase 1: evaluate + rank t_k (data waves)
+    if (!control && have) { WX_EVAL_AND_RANK(s_cnt[buf]) }
     __syncthreads();
-
-    const wx_i64 next = tile + tile_step;
-#if WX_COMPACT_PREFETCH
-    if (next < wx_a.n_tiles) {
-      const wx_i64 wx_tb = next * WX_TILE;
-#pragma unroll
-      for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
-    }
-#endif
-
-    wx_u32 grp_base[WX_GROUPS];
+    // phase 2: control publishes t_k's aggregate; data waves stage t_k and prefetch t_{k+1}
     wx_u32 block_total = 0;
+    wx_u32 grp_base[WX_GROUPS];
+    if (have) { WX_BASES(s_cnt[buf]) }
+    if (control) {
+      if (have && lane == 0)
+        wx::st_agent(&wx_a.status[tile], (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
+    } else if (have) {
 #pragma unroll
-    for (int g = 0; g < WX_GROUPS; ++g) {
-      wx_u32 before = 0, gsum = 0;
+      for (int g = 0; g < WX_GROUPS; ++g) {
+        wx_u32 pos = grp_base[g] + lane_pre[g];
 #pragma unroll
-      for (int w = 0; w < WX_WAVES; ++w) {
-        const wx_u32 c = s_wave_cnt[w][g];
-        before += (w < wave) ? c : 0u;
-        gsum += c;
-      }
-      grp_base[g] = block_total + before;
-      block_total += gsum;
-    }
-
-    if (wave == 0) {
-      wx_i64 excl = 0;
-#if WX_DIAG_NO_LOOKBACK
-      excl = tile_base / 2;  // diagnostic build: timing only, results invalid
-#else
-      if (tile == 0) {
-        if (lane == 0) wx::st_agent(&wx_a.status[0], WX_FLAG_P | (wx_u64)block_total);
-      } else {
-        if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_A | (wx_u64)block_total);
-        excl = wx_lookback(wx_a, tile);
-        if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_P | (wx_u64)(excl + block_total));
-      }
-#endif
-      if (lane == 0) s_excl = excl;
-    }
-    __syncthreads();
-    const wx_i64 excl = s_excl;
-
-#if WX_DIAG_NO_STORE
-    float sink = 0.0f;
-#pragma unroll
-    for (int g = 0; g < WX_GROUPS; ++g)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) sink += wx_keep[g][e] ? wx_val[g][e] + (float)(excl + grp_base[g] + lane_pre[g]) : 0.0f;
-    if (sink == -1.0f && wx_a.out_val) wx_a.out_val[0] = sink;  // keeps the work alive
-#else
-#pragma unroll
-    for (int g = 0; g < WX_GROUPS; ++g) {
-      const wx_i64 r0 = tile_base + (wx_i64)g * (WX_BLOCK * 4) + (wx_i64)tid * 4;
-      wx_i64 pos = excl + grp_base[g] + lane_pre[g];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        if (wx_keep[g][e]) {
-          if (wx_a.out_val) wx_a.out_val[pos] = wx_val[g][e];
-          if (wx_a.out_idx) {
-            const wx_i64 gi = wx_a.row_base + r0 + e;
-            if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
-            else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
+        for (int e = 0; e < 4; ++e) {
+          if (wx_keep[g][e]) {
+            s_val[buf][pos] = wx_val[g][e];
+            s_off[buf][pos] = (unsigned short)(g * (WX_BLOCK * 4) + wx_dt * 4 + e);
+            ++pos;
           }
-          ++pos;
         }
       }
-    }
-#endif
-    if (tid == 0 && tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
-#if !WX_COMPACT_PREFETCH
-    if (next < wx_a.n_tiles) {
-      const wx_i64 wx_tb = next * WX_TILE;
+      const wx_i64 next = tile + grid;
+      if (next < wx_a.n_tiles) {
+        const wx_i64 wx_tb = next * WX_TILE;
 #pragma unroll
-      for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
+        for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
+      }
     }
+    __syncthreads();
+    // phase 3: control resolves t_k's offset; data waves write out t_{k-1}
+    if (control) {
+      if (have) {
+        wx_i64 excl = 0;
+#if WX_DIAG_NO_LOOKBACK
+        excl = tile_base / 2;  // diagnostic build: timing only, results invalid
+#else
+        if (tile > 0) {
+          excl = wx_lookback(wx_a, tile);
+          if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_P | (wx_u64)(excl + block_total));
+        }
 #endif
-    tile = next;
+        if (lane == 0) {
+          s_excl[buf] = excl;
+          if (tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
+        }
+      }
+    } else if (have_prev) {
+      const int pb = buf ^ 1;
+      const wx_i64 excl = s_excl[pb];
+      const wx_i64 prev_base = wx_a.row_base + (tile - grid) * WX_TILE;
+#if !WX_DIAG_NO_STORE
+      for (int i = wx_dt; i < (int)prev_total; i += WX_BLOCK) {
+        const wx_i64 pos = excl + i;
+        if (wx_a.out_val) wx_a.out_val[pos] = s_val[pb][i];
+        if (wx_a.out_idx) {
+          const wx_i64 gi = prev_base + s_off[pb][i];
+          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
+          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
+        }
+      }
+#else
+      if (excl == -1 && wx_a.out_val) wx_a.out_val[0] = s_val[pb][wx_dt];
+#endif
+    }
+    prev_total = block_total;
+    tile += grid;
   }
+}
+
+// One tile per workgroup, taken from a ticket counter (robust fallback).
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_compact_ticket(WxCompactArgs wx_a) {
+  __shared__ wx_u32 s_cnt[WX_WAVES][WX_GROUPS];
+  __shared__ wx_i64 s_excl;
+  __shared__ wx_u32 s_tile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wx_dt = tid;
+  if (tid == 0)
+    s_tile = (wx_u32)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const wx_i64 tile = s_tile;
+  const wx_i64 tile_base = tile * WX_TILE;
+  WX_COLS(WX_DECL_TILE_IN)
+  {
+    const wx_i64 wx_tb = tile_base;
+#pragma unroll
+    for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
+  }
+  bool wx_keep[WX_GROUPS][4];
+  float wx_val[WX_GROUPS][4];
+  wx_u32 lane_pre[WX_GROUPS];
+  WX_EVAL_AND_RANK(s_cnt)
+  __syncthreads();
+  wx_u32 block_total = 0;
+  wx_u32 grp_base[WX_GROUPS];
+  WX_BASES(s_cnt)
+  if (wave == 0) {
+    wx_i64 excl = 0;
+    if (tile == 0) {
+      if (lane == 0) wx::st_agent(&wx_a.status[0], WX_FLAG_P | (wx_u64)block_total);
+    } else {
+      if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_A | (wx_u64)block_total);
+      excl = wx_lookback(wx_a, tile);
+      if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_P | (wx_u64)(excl + block_total));
+    }
+    if (lane == 0) s_excl = excl;
+  }
+  __syncthreads();
+  const wx_i64 excl = s_excl;
+#pragma unroll
+  for (int g = 0; g < WX_GROUPS; ++g) {
+    const wx_i64 r0 = tile_base + (wx_i64)g * (WX_BLOCK * 4) + (wx_i64)tid * 4;
+    wx_i64 pos = excl + grp_base[g] + lane_pre[g];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      if (wx_keep[g][e]) {
+        if (wx_a.out_val) wx_a.out_val[pos] = wx_val[g][e];
+        if (wx_a.out_idx) {
+          const wx_i64 gi = wx_a.row_base + r0 + e;
+          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
+          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
+        }
+        ++pos;
+      }
+    }
+  }
+  if (tid == 0 && tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
 }
 #endif
 
