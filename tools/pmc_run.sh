@@ -1,0 +1,16 @@
+#!/usr/bin/env bash
+# PMC traffic passes for one bench workload (GPU box).  FETCH_SIZE and
+# WRITE_SIZE go in separate rocprofv3 passes (TCC slots), kernel trace only.
+set -euo pipefail
+W=${1:-project}
+ROWS=${2:-1e9}
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/pmc_$W
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+for C in FETCH_SIZE WRITE_SIZE; do
+  timeout -k 10 300 rocprofv3 --pmc $C -d "$OUT/$C" -o run --output-format csv -- \
+    python3 "$R/bench.py" --workload "$W" --rows "$ROWS" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/$C.log" 2>&1
+done
+python3 "$R/tools/pmc_summary.py" $(find "$OUT" -name "*counter_collection.csv") > "$OUT/summary.json"
+cat "$OUT/summary.json"
