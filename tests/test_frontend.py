@@ -1,0 +1,102 @@
+"""CPU tests of the product front end (libwarpdb via pywarpdb): lowering,
+tokenizer and error messages against the reference's goldens
+(tests/golden/golden.json, produced from the reference's own parser) and the
+expectations of the reference's unit tests."""
+from __future__ import annotations
+
+import json
+import os
+
+import pytest
+
+from warpdb_amd import pywarpdb as pw
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def golden():
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)
+
+
+@pytest.mark.parametrize("case", golden()["lower"], ids=lambda c: c["expr"])
+def test_lowering_matches_reference(case):
+    assert pw.lower_expression(case["expr"]) == case["lowered"]
+
+
+@pytest.mark.parametrize("case", golden()["errors"], ids=lambda c: repr(c["expr"]))
+def test_errors_match_reference(case):
+    with pytest.raises(RuntimeError) as ei:
+        pw.lower_expression(case["expr"])
+    assert str(ei.value) == case["message"].replace("ERROR: ", "")
+
+
+def test_tokenizer_expectations():
+    # tests/tokenizer_tests.cpp
+    toks = pw.tokenize("price > 10")
+    assert [(t[0], t[1]) for t in toks] == [(0, "price"), (2, ">"), (1, "10"), (4, "")]
+    kinds = [t[0] for t in pw.tokenize("(price + 5) * quantity")]
+    assert kinds == [2, 0, 2, 1, 2, 2, 0, 4]
+    vals = [t[1] for t in pw.tokenize("price > 10 AND quantity < 5") if t[0] == 3]
+    assert vals == ["AND"]
+    toks = pw.tokenize("a >= 1 != 2\n  b")
+    assert [t[1] for t in toks][:5] == ["a", ">=", "1", "!=", "2"]
+    assert toks[5][2:] == (2, 3)  # line / column tracking
+
+
+def test_equality_is_not_assignment():
+    # deviation: the reference lowers '=' to a C assignment
+    assert pw.lower_expression("quantity = 7") == "(quantity[idx] == 7.0f)"
+
+
+def test_split_where():
+    assert pw.split_where("price * quantity WHERE price > 10") == ("price * quantity ", " price > 10")
+    assert pw.split_where("price where price > 1") == ("price ", " price > 1")
+    assert pw.split_where("price") == ("price", "")
+
+
+def test_parse_query_reference_cases():
+    # tests/query_parser_test.cpp
+    q = pw.parse_query_summary("SELECT SUM(price), quantity FROM sales JOIN items ON sales.id = items.id "
+                               "WHERE price > 10 GROUP BY quantity ORDER BY price DESC LIMIT 5")
+    assert len(q["select"]) == 2 and q["joins"] == 1 and q["where"] and q["group_by"] == 1
+    assert q["order_by"] == ("price[idx]", False) and q["limit"] == 5
+    # tests/parse_query_error_test.cpp: message carries line and column
+    with pytest.raises(RuntimeError, match="line 1 column"):
+        pw.parse_query_summary("SELECT price")
+    # tests/parsing_error_tests.cpp
+    with pytest.raises(RuntimeError, match="Unexpected token"):
+        pw.parse_query_summary("SELECT price FROM test EXTRA")
+    # tests/sql_features_test.cpp shapes
+    q = pw.parse_query_summary("SELECT price FROM test ORDER BY price DESC OFFSET 1 LIMIT 2")
+    assert q["offset"] == 1 and q["limit"] == 2
+    q = pw.parse_query_summary("SELECT SUM(price) FROM test GROUP BY quantity HAVING SUM(price) > 15 "
+                               "ORDER BY quantity ASC")
+    assert q["having"] == "(price[idx] > 15.0f)" and q["order_by"] == ("quantity[idx]", True)
+    q = pw.parse_query_summary("SELECT DISTINCT quantity FROM test ORDER BY quantity DESC")
+    assert q["distinct"]
+    q = pw.parse_query_summary("SELECT COUNT(*) FROM t WHERE price > 1")
+    assert q["select"] == ["1.0f"]
+
+
+def test_plan_shards_matches_reference_partition():
+    # ceil(N / devices) contiguous rows (src/multi_gpu_utils.cpp:24-32)
+    assert pw.plan_shards(10, 4) == [(0, 0, 3), (1, 3, 6), (2, 6, 9), (3, 9, 10)]
+    assert pw.plan_shards(3, 8) == [(0, 0, 1), (1, 1, 2), (2, 2, 3)]
+    assert pw.plan_shards(0, 8) == []
+    n = 8_000_000_000
+    s = pw.plan_shards(n, 8)
+    assert len(s) == 8 and s[-1][2] == n and all(e - b == 1_000_000_000 for _, b, e in s)
+
+
+def test_cpp_frontend_binary():
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "-C", os.path.join(root, "tests", "cpp"), "frontend_test"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([os.path.join(root, "tests", "cpp", "bin", "frontend_test")], capture_output=True,
+                       text=True, cwd=root)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "frontend_test: all passed" in r.stdout

@@ -1,0 +1,110 @@
+// pywarpdb.cpp -- Python module with the reference's binding surface
+// (bindings/python/pywarpdb.cpp:7-38): WarpDB(path), query, query_multi_gpu,
+// query_multi_gpu_csv (static), query_arrow -> (array capsule, schema
+// capsule); plus query_sql / query_compact / query_sum and the front end.
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include "warpdb/multi_gpu_utils.hpp"
+#include "warpdb/warpdb.hpp"
+
+namespace py = pybind11;
+
+namespace {
+py::tuple arrow_capsules(ArrowArray *arr, ArrowSchema *schema) {
+  py::capsule a(arr, [](void *p) {
+    auto *x = static_cast<ArrowArray *>(p);
+    if (x->release) x->release(x);
+    delete x;
+  });
+  py::capsule s(schema, [](void *p) {
+    auto *x = static_cast<ArrowSchema *>(p);
+    if (x->release) x->release(x);
+    delete x;
+  });
+  return py::make_tuple(a, s);
+}
+}  // namespace
+
+PYBIND11_MODULE(pywarpdb, m) {
+  m.doc() = "WarpDB query engine on AMD Instinct MI355X (hiprtc + gfx950 kernels)";
+  py::enum_<DataType>(m, "DataType")
+      .value("Int32", DataType::Int32)
+      .value("Int64", DataType::Int64)
+      .value("Float32", DataType::Float32)
+      .value("Float64", DataType::Float64)
+      .value("String", DataType::String);
+
+  py::class_<WarpDB>(m, "WarpDB")
+      .def(py::init<const std::string &>())
+      .def(py::init<const std::string &, const std::vector<DataType> &, int>(), py::arg("path"), py::arg("schema"),
+           py::arg("device") = 0)
+      .def("query", &WarpDB::query, py::call_guard<py::gil_scoped_release>())
+      .def("query_sql", &WarpDB::query_sql, py::call_guard<py::gil_scoped_release>())
+      .def("query_multi_gpu", &WarpDB::query_multi_gpu, py::arg("expr"), py::call_guard<py::gil_scoped_release>(),
+           "Execute expression using all available GPUs on the current table.")
+      .def_static("query_multi_gpu_csv", &WarpDB::query_multi_gpu_csv, py::arg("csv_path"), py::arg("expr"),
+                  py::arg("rows_per_chunk") = 1000000, py::call_guard<py::gil_scoped_release>(),
+                  "Stream a CSV file in chunks across all GPUs and return results.")
+      .def(
+          "query_arrow",
+          [](WarpDB &db, const std::string &expr, bool shared_memory) {
+            auto *arr = new ArrowArray();
+            auto *schema = new ArrowSchema();
+            try {
+              db.query_arrow(expr, arr, schema, shared_memory);
+            } catch (...) {
+              delete arr;
+              delete schema;
+              throw;
+            }
+            return arrow_capsules(arr, schema);
+          },
+          py::arg("expr"), py::arg("shared_memory") = false,
+          "Return result as Arrow C Data Interface capsules (ArrowArray, ArrowSchema).")
+      .def("query_compact", &WarpDB::query_compact, py::call_guard<py::gil_scoped_release>())
+      .def("query_sum", &WarpDB::query_sum, py::call_guard<py::gil_scoped_release>())
+      .def("query_multi_gpu_sum", &WarpDB::query_multi_gpu_sum, py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("num_rows", [](const WarpDB &db) { return db.table().num_rows; })
+      .def_property_readonly("column_names", [](const WarpDB &db) {
+        std::vector<std::string> n;
+        for (const auto &c : db.table().columns) n.push_back(c.name);
+        return n;
+      });
+
+  // front end, for tests and tools
+  m.def("lower_expression", [](const std::string &e) { return parse_expression(tokenize(e))->to_cuda_expr(); });
+  m.def("split_where", [](const std::string &q) {
+    std::string e, c;
+    warpdb::split_where(q, e, c);
+    return py::make_tuple(e, c);
+  });
+  m.def("tokenize", [](const std::string &s) {
+    py::list out;
+    for (const auto &t : tokenize(s)) out.append(py::make_tuple(static_cast<int>(t.type), t.value, t.line, t.column));
+    return out;
+  });
+  m.def("parse_query_summary", [](const std::string &sql) {
+    QueryAST q = parse_query(tokenize(sql));
+    py::dict d;
+    py::list sel;
+    for (const auto &e : q.select_list) sel.append(e->to_cuda_expr());
+    d["select"] = sel;
+    d["from"] = q.from_table;
+    d["joins"] = q.joins.size();
+    d["where"] = q.where ? py::object(py::str((*q.where)->to_cuda_expr())) : py::none();
+    d["group_by"] = q.group_by ? py::object(py::int_(q.group_by->keys.size())) : py::none();
+    d["having"] = q.having ? py::object(py::str((*q.having)->to_cuda_expr())) : py::none();
+    d["order_by"] = q.order_by ? py::object(py::make_tuple(q.order_by->expr->to_cuda_expr(), q.order_by->ascending))
+                               : py::none();
+    d["limit"] = q.limit ? py::object(py::int_(q.limit->count)) : py::none();
+    d["offset"] = q.offset ? py::object(py::int_(q.offset->count)) : py::none();
+    d["distinct"] = q.distinct;
+    return d;
+  });
+  m.def("plan_shards", [](int64_t n, int devices) {
+    py::list out;
+    for (auto &s : warpdb::plan_shards(n, devices)) out.append(py::make_tuple(s.device, s.begin, s.end));
+    return out;
+  });
+}

@@ -1,0 +1,410 @@
+// warpdb.cpp -- the WarpDB facade on the MI355X execution layer.
+// Reference: src/warpdb.cpp:159-590.  query() keeps the reference's result
+// contract (dense vector of num_rows floats); the work runs through the C
+// ABI (include/warpexec.h) on the table resident in HBM.
+#include "warpdb/warpdb.hpp"
+
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <cctype>
+#include <cmath>
+#include <fstream>
+#include <functional>
+#include <map>
+#include <sstream>
+#include <stdexcept>
+#include <unordered_set>
+
+#include "warpdb/internal.hpp"
+#include "warpdb/multi_gpu_utils.hpp"
+
+using warpdb::DeviceBuffer;
+using warpdb::DevGuard;
+using warpdb::hip_ok;
+using warpdb::sync_launch;
+using warpdb::throw_on;
+using warpdb::WxTableView;
+
+namespace {
+
+// Every column reference must name a table column (src/warpdb.cpp:19-44).
+void validate_ast(const ASTNode *node, const std::unordered_set<std::string> &cols) {
+  if (!node) return;
+  if (auto v = dynamic_cast<const VariableNode *>(node)) {
+    if (!cols.count(v->name)) throw std::runtime_error("Unknown column: " + v->name);
+  } else if (auto b = dynamic_cast<const BinaryOpNode *>(node)) {
+    validate_ast(b->left.get(), cols);
+    validate_ast(b->right.get(), cols);
+  } else if (auto f = dynamic_cast<const FunctionCallNode *>(node)) {
+    for (const auto &a : f->args) validate_ast(a.get(), cols);
+  } else if (auto a = dynamic_cast<const AggregationNode *>(node)) {
+    validate_ast(a->expr.get(), cols);
+  } else if (auto w = dynamic_cast<const WindowFunctionNode *>(node)) {
+    validate_ast(w->expr.get(), cols);
+    for (const auto &p : w->partition_by) validate_ast(p.get(), cols);
+    if (w->order_by) validate_ast(w->order_by->expr.get(), cols);
+  }
+}
+
+std::unordered_set<std::string> names_of(const Table &t) {
+  std::unordered_set<std::string> s;
+  for (const auto &c : t.columns) s.insert(c.name);
+  return s;
+}
+
+std::unordered_set<std::string> names_of(const HostTable &t) {
+  std::unordered_set<std::string> s;
+  for (const auto &c : t.columns) s.insert(c.name);
+  return s;
+}
+
+bool blank(const std::string &s) {
+  return std::all_of(s.begin(), s.end(), [](char c) { return std::isspace(static_cast<unsigned char>(c)); });
+}
+
+// split + parse + validate + lower, with the reference's error prefixes
+void lower_query(const std::string &query, const std::unordered_set<std::string> &cols, std::string &expr_c,
+                 std::string &cond_c) {
+  if (query.empty()) throw std::runtime_error("Empty query expression");
+  std::string e, c;
+  warpdb::split_where(query, e, c);
+  ASTNodePtr ex;
+  try {
+    ex = parse_expression(tokenize(e));
+  } catch (const std::exception &err) {
+    throw std::runtime_error(std::string("Failed to parse expression: ") + err.what());
+  }
+  validate_ast(ex.get(), cols);
+  expr_c = ex->to_cuda_expr();
+  cond_c.clear();
+  if (!blank(c)) {
+    try {
+      auto cx = parse_expression(tokenize(c));
+      validate_ast(cx.get(), cols);
+      cond_c = cx->to_cuda_expr();
+    } catch (const std::exception &err) {
+      throw std::runtime_error(std::string("Failed to parse WHERE clause: ") + err.what());
+    }
+  }
+}
+
+std::string lower_ext(const std::string &path) {
+  const auto dot = path.find_last_of('.');
+  std::string ext = dot == std::string::npos ? "" : path.substr(dot + 1);
+  for (char &ch : ext) ch = static_cast<char>(std::tolower(static_cast<unsigned char>(ch)));
+  return ext;
+}
+
+std::vector<float> download(const void *d, int64_t n, int device) {
+  std::vector<float> h(static_cast<size_t>(n));
+  DevGuard g(device);
+  if (n) hip_ok(hipMemcpy(h.data(), d, sizeof(float) * static_cast<size_t>(n), hipMemcpyDeviceToHost), "hipMemcpy");
+  return h;
+}
+
+bool same_expr(const ASTNode *a, const ASTNode *b) { return a && b && a->to_cuda_expr() == b->to_cuda_expr(); }
+
+}  // namespace
+
+WarpDB::WarpDB(const std::string &filepath, const std::vector<DataType> &schema, int device) {
+  const std::string ext = lower_ext(filepath);
+  if (ext == "csv") {
+    host_table_ = load_csv_to_host(filepath, schema);
+  } else if (ext == "json") {
+    host_table_ = load_json_to_host(filepath);
+  } else if (ext == "parquet" || ext == "arrow" || ext == "feather" || ext == "orc") {
+    throw std::runtime_error("Arrow support is not compiled into WarpDB");
+  } else {
+    throw std::runtime_error("Unsupported file format: " + filepath);
+  }
+  table_ = upload_to_gpu(host_table_, device);
+}
+
+WarpDB::~WarpDB() { free_table(table_); }
+
+void WarpDB::lower(const std::string &query, std::string &expr_c, std::string &cond_c) const {
+  lower_query(query, names_of(table_), expr_c, cond_c);
+}
+
+std::vector<float> WarpDB::query(const std::string &expr) {
+  std::string e, c;
+  lower(expr, e, c);
+  const int64_t n = table_.num_rows;
+  DeviceBuffer out(table_.device, sizeof(float) * static_cast<size_t>(n ? n : 1));
+  WxTableView v(table_);
+  wx_launch L = sync_launch(table_.device);
+  char err[8192];
+  throw_on(wx_project_filter(&v.table, e.c_str(), c.c_str(), &L, WX_MODE_DENSE_FILL, static_cast<float *>(out.ptr),
+                             nullptr, 0, 0, nullptr, nullptr, err, sizeof(err)),
+           err);
+  return download(out.ptr, n, table_.device);
+}
+
+std::pair<std::vector<float>, std::vector<int64_t>> WarpDB::query_compact(const std::string &expr) {
+  std::string e, c;
+  lower(expr, e, c);
+  const int64_t n = table_.num_rows;
+  DeviceBuffer vals(table_.device, sizeof(float) * static_cast<size_t>(n ? n : 1));
+  DeviceBuffer idx(table_.device, sizeof(int64_t) * static_cast<size_t>(n ? n : 1));
+  WxTableView v(table_);
+  wx_launch L = sync_launch(table_.device);
+  int64_t count = 0;
+  char err[8192];
+  throw_on(wx_project_filter(&v.table, e.c_str(), c.c_str(), &L, WX_MODE_COMPACT, static_cast<float *>(vals.ptr),
+                             idx.ptr, 8, 0, nullptr, &count, err, sizeof(err)),
+           err);
+  std::vector<float> hv = download(vals.ptr, count, table_.device);
+  std::vector<int64_t> hi(static_cast<size_t>(count));
+  DevGuard g(table_.device);
+  if (count) hip_ok(hipMemcpy(hi.data(), idx.ptr, sizeof(int64_t) * count, hipMemcpyDeviceToHost), "hipMemcpy");
+  return {std::move(hv), std::move(hi)};
+}
+
+std::pair<double, int64_t> WarpDB::query_sum(const std::string &expr) {
+  std::string e, c;
+  lower(expr, e, c);
+  WxTableView v(table_);
+  wx_launch L = sync_launch(table_.device);
+  double s = 0;
+  int64_t n = 0;
+  char err[8192];
+  throw_on(wx_reduce_sum(&v.table, e.c_str(), c.c_str(), &L, nullptr, &s, &n, err, sizeof(err)), err);
+  return {s, n};
+}
+
+void WarpDB::query_arrow(const std::string &expr, ArrowArray *out_array, ArrowSchema *out_schema,
+                         bool use_shared_memory) {
+  auto r = query(expr);
+  export_to_arrow(r.data(), static_cast<int64_t>(r.size()), use_shared_memory, out_array, out_schema);
+}
+
+void WarpDB::query_arrow_device(const std::string &expr, ArrowDeviceArray *out_array, ArrowSchema *out_schema) {
+  std::string e, c;
+  lower(expr, e, c);
+  const int64_t n = table_.num_rows;
+  DeviceBuffer out(table_.device, sizeof(float) * static_cast<size_t>(n ? n : 1));
+  WxTableView v(table_);
+  wx_launch L = sync_launch(table_.device);
+  char err[8192];
+  throw_on(wx_project_filter(&v.table, e.c_str(), c.c_str(), &L, WX_MODE_DENSE_FILL, static_cast<float *>(out.ptr),
+                             nullptr, 0, 0, nullptr, nullptr, err, sizeof(err)),
+           err);
+  const int dev = table_.device;
+  export_device_to_arrow(static_cast<float *>(out.release()), n, dev, out_array, out_schema);
+}
+
+std::vector<float> WarpDB::query_multi_gpu(const std::string &expr) {
+  if (host_table_.num_rows() == 0) throw std::runtime_error("Host table not available for multi-GPU query");
+  std::string e, c;
+  lower_query(expr, names_of(host_table_), e, c);
+  return run_multi_gpu_jit_host(host_table_, e, c);
+}
+
+std::pair<double, int64_t> WarpDB::query_multi_gpu_sum(const std::string &expr) {
+  if (host_table_.num_rows() == 0) throw std::runtime_error("Host table not available for multi-GPU query");
+  std::string e, c;
+  lower_query(expr, names_of(host_table_), e, c);
+  return warpdb::run_multi_gpu_sum(host_table_, e, c);
+}
+
+std::vector<float> WarpDB::query_multi_gpu_csv(const std::string &csv_path, const std::string &expr,
+                                               int rows_per_chunk) {
+  if (rows_per_chunk <= 0) throw std::runtime_error("rows_per_chunk must be positive");
+  std::ifstream file(csv_path);
+  if (!file.is_open()) throw std::runtime_error("Failed to open file: " + csv_path);
+  std::string header;
+  if (!std::getline(file, header)) throw std::runtime_error("Empty CSV file");
+  if (!header.empty() && header.back() == '\r') header.pop_back();
+  std::vector<std::string> names;
+  {
+    std::stringstream ss(header);
+    std::string n;
+    while (std::getline(ss, n, ',')) names.push_back(n);
+  }
+  std::unordered_set<std::string> cols(names.begin(), names.end());
+  std::string e, c;
+  lower_query(expr, cols, e, c);
+  std::vector<float> all;
+  bool finished = false;
+  while (!finished) {
+    HostTable chunk = load_csv_chunk(file, static_cast<int64_t>(rows_per_chunk), finished, names);
+    if (chunk.num_rows() == 0) break;
+    auto part = run_multi_gpu_jit_host(chunk, e, c);
+    all.insert(all.end(), part.begin(), part.end());
+  }
+  return all;
+}
+
+// ------------------------------------------------------------------ SQL
+std::vector<float> WarpDB::query_sql(const std::string &sql) {
+  QueryAST ast;
+  try {
+    ast = parse_query(tokenize(sql));
+  } catch (const std::exception &e) {
+    throw std::runtime_error(std::string("Failed to parse SQL: ") + e.what());
+  }
+  const auto cols = names_of(table_);
+  auto validate_ctx = [&](const ASTNode *n, const std::string &ctx) {
+    try {
+      validate_ast(n, cols);
+    } catch (const std::exception &e) {
+      throw std::runtime_error(ctx + ": " + e.what());
+    }
+  };
+  if (ast.select_list.empty()) throw std::runtime_error("Empty SELECT list");
+  for (const auto &e : ast.select_list) validate_ctx(e.get(), "SELECT clause");
+  for (const auto &j : ast.joins) validate_ctx(j.condition.get(), "JOIN condition");
+  if (ast.where) validate_ctx(ast.where->get(), "WHERE clause");
+  if (ast.group_by)
+    for (const auto &k : ast.group_by->keys) validate_ctx(k.get(), "GROUP BY");
+  if (ast.order_by) validate_ctx(ast.order_by->expr.get(), "ORDER BY");
+  if (!ast.joins.empty()) throw std::runtime_error("JOIN is not supported by the execution engine");
+
+  const std::string cond = ast.where ? (*ast.where)->to_cuda_expr() : std::string();
+  WxTableView v(table_);
+  wx_launch L = sync_launch(table_.device);
+  char err[8192];
+  std::vector<float> result;
+  const size_t off = ast.offset ? static_cast<size_t>(std::max(0, ast.offset->count)) : 0;
+  const size_t lim = ast.limit ? static_cast<size_t>(std::max(0, ast.limit->count)) : SIZE_MAX;
+  auto slice = [&](std::vector<float> r) {
+    if (off >= r.size()) return std::vector<float>();
+    r.erase(r.begin(), r.begin() + static_cast<long>(off));
+    if (r.size() > lim) r.resize(lim);
+    return r;
+  };
+  auto *agg = dynamic_cast<const AggregationNode *>(ast.select_list[0].get());
+
+  if (ast.group_by) {
+    if (!agg) throw std::runtime_error("Only aggregation queries supported with GROUP BY");
+    if (ast.group_by->keys.size() != 1) throw std::runtime_error("GROUP BY supports one key expression");
+    const ASTNode *key = ast.group_by->keys[0].get();
+    const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(table_.num_rows, 1 << 22));
+    DeviceBuffer dk(table_.device, cap * 4), ds(table_.device, cap * 8), dc(table_.device, cap * 8);
+    int64_t g = 0;
+    throw_on(wx_group_sum(&v.table, agg->expr->to_cuda_expr().c_str(), key->to_cuda_expr().c_str(), cond.c_str(), &L,
+                          0, cap, static_cast<int32_t *>(dk.ptr), static_cast<double *>(ds.ptr),
+                          static_cast<int64_t *>(dc.ptr), nullptr, &g, err, sizeof(err)),
+             err);
+    std::vector<int32_t> keys(g);
+    std::vector<double> sums(g);
+    std::vector<int64_t> cnts(g);
+    {
+      DevGuard dg(table_.device);
+      if (g) {
+        hip_ok(hipMemcpy(keys.data(), dk.ptr, g * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+        hip_ok(hipMemcpy(sums.data(), ds.ptr, g * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+        hip_ok(hipMemcpy(cnts.data(), dc.ptr, g * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+      }
+    }
+    // per-group aggregate value; MIN / MAX need reducers the engine lacks
+    auto value_of = [&](AggregationType t, size_t i) -> double {
+      switch (t) {
+        case AggregationType::Sum: return sums[i];
+        case AggregationType::Avg: return sums[i] / static_cast<double>(cnts[i]);
+        case AggregationType::Count: return static_cast<double>(cnts[i]);
+        default: throw std::runtime_error("MIN/MAX aggregation is not supported by the execution engine");
+      }
+    };
+    // HAVING over the (few) aggregated groups, with the reference's
+    // comparison semantics (src/warpdb.cpp:387-423)
+    std::function<double(const ASTNode *, size_t)> having = [&](const ASTNode *n, size_t i) -> double {
+      if (auto c = dynamic_cast<const ConstantNode *>(n)) return std::stod(c->value);
+      if (auto a = dynamic_cast<const AggregationNode *>(n)) {
+        if (!same_expr(a->expr.get(), agg->expr.get()) && a->agg != AggregationType::Count)
+          throw std::runtime_error("HAVING may only aggregate the selected expression");
+        return value_of(a->agg, i);
+      }
+      if (auto b = dynamic_cast<const BinaryOpNode *>(n)) {
+        const double l = having(b->left.get(), i), r = having(b->right.get(), i);
+        const std::string &op = b->op;
+        if (op == "+") return l + r;
+        if (op == "-") return l - r;
+        if (op == "*") return l * r;
+        if (op == "/") return l / r;
+        if (op == ">") return l > r;
+        if (op == "<") return l < r;
+        if (op == ">=") return l >= r;
+        if (op == "<=") return l <= r;
+        if (op == "==") return l == r;
+        if (op == "!=") return l != r;
+        if (op == "&&") return l != 0 && r != 0;
+        if (op == "||") return l != 0 || r != 0;
+      }
+      if (same_expr(n, key)) return keys[i];
+      throw std::runtime_error("unsupported HAVING term");
+    };
+    std::vector<size_t> order;
+    for (size_t i = 0; i < static_cast<size_t>(g); ++i)
+      if (!ast.having || having(ast.having->get(), i) != 0.0) order.push_back(i);
+    if (ast.order_by) {  // groups arrive in ascending key order
+      const ASTNode *ob = ast.order_by->expr.get();
+      auto *oagg = dynamic_cast<const AggregationNode *>(ob);
+      if (oagg) {
+        std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) {
+          const double x = value_of(oagg->agg, a), y = value_of(oagg->agg, b);
+          return ast.order_by->ascending ? x < y : x > y;
+        });
+      } else if (same_expr(ob, key)) {
+        if (!ast.order_by->ascending) std::reverse(order.begin(), order.end());
+      } else {
+        throw std::runtime_error("ORDER BY with GROUP BY must name the key or an aggregate");
+      }
+    }
+    for (size_t i : order) result.push_back(static_cast<float>(value_of(agg->agg, i)));
+    if (ast.distinct) {
+      std::sort(result.begin(), result.end());
+      result.erase(std::unique(result.begin(), result.end()), result.end());
+    }
+    return slice(std::move(result));
+  }
+
+  if (agg) {  // ungrouped aggregate over the WHERE rows
+    double s = 0;
+    int64_t n = 0;
+    throw_on(wx_reduce_sum(&v.table, agg->expr->to_cuda_expr().c_str(), cond.c_str(), &L, nullptr, &s, &n, err,
+                           sizeof(err)),
+             err);
+    double val;
+    switch (agg->agg) {
+      case AggregationType::Sum: val = s; break;
+      case AggregationType::Avg: val = n ? s / n : NAN; break;
+      case AggregationType::Count: val = static_cast<double>(n); break;
+      default: throw std::runtime_error("MIN/MAX aggregation is not supported by the execution engine");
+    }
+    return slice({static_cast<float>(val)});
+  }
+
+  const ASTNode *sel = ast.select_list[0].get();
+  const std::string sel_c = sel->to_cuda_expr();
+  const ASTNode *ob = ast.order_by ? ast.order_by->expr.get() : nullptr;
+  // ORDER BY .. LIMIT k: device top-K (ties by ascending row index)
+  if (ob && !ast.distinct && ast.limit && off + lim <= 32) {
+    const int k = static_cast<int>(off + lim);
+    if (k == 0) return {};
+    DeviceBuffer dv(table_.device, sizeof(float) * k);
+    int64_t m = 0;
+    throw_on(wx_topk(&v.table, ob->to_cuda_expr().c_str(), cond.c_str(), sel_c.c_str(), k,
+                     ast.order_by->ascending ? 0 : 1, &L, 0, nullptr, nullptr, static_cast<float *>(dv.ptr), nullptr,
+                     &m, err, sizeof(err)),
+             err);
+    return slice(download(dv.ptr, m, table_.device));
+  }
+  // projection of the WHERE rows in row order (ordered compaction)
+  const int64_t n = table_.num_rows;
+  DeviceBuffer dv(table_.device, sizeof(float) * static_cast<size_t>(n ? n : 1));
+  int64_t count = 0;
+  throw_on(wx_project_filter(&v.table, sel_c.c_str(), cond.c_str(), &L, WX_MODE_COMPACT, static_cast<float *>(dv.ptr),
+                             nullptr, 0, 0, nullptr, &count, err, sizeof(err)),
+           err);
+  if (ob || ast.distinct) {
+    if (ob && !same_expr(ob, sel))
+      throw std::runtime_error("ORDER BY a different expression needs LIMIT + OFFSET <= 32");
+    const bool asc = ob ? ast.order_by->ascending : true;
+    throw_on(wx_sort_float(static_cast<float *>(dv.ptr), count, asc ? 1 : 0, &L, err, sizeof(err)), err);
+  }
+  result = download(dv.ptr, count, table_.device);
+  if (ast.distinct) result.erase(std::unique(result.begin(), result.end()), result.end());
+  return slice(std::move(result));
+}
