@@ -32,19 +32,18 @@ cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
 ref_count = int((price > 15.0).sum().item())
 
 VARIANTS = {
-    "pipe_g4_lb2": {},
-    "pipe_g4_lb1": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=1"},
-    "pipe_g4_lb4": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=4"},
-    "pipe_g4_lb8": {"WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=8"},
-    "pipe_g4_lb2_sl0": {"WARPDB_EXTRA_DEFINES": "WX_LB_SLEEP=0"},
-    "pipe_g4_lb2_sl8": {"WARPDB_EXTRA_DEFINES": "WX_LB_SLEEP=8"},
-    "ticket_g4_lb2": {"WARPDB_COMPACT_SCHED": "ticket"},
-    "pipe_g4_nolookback": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK"},
+    "dw8_g4": {},
+    "dw12_g4": {"WARPDB_COMPACT_DWAVES": "12"},
+    "dw15_g4": {"WARPDB_COMPACT_DWAVES": "15"},
+    "dw12_g6": {"WARPDB_COMPACT_DWAVES": "12", "WARPDB_COMPACT_GROUPS": "6"},
+    "dw15_g4_lb2": {"WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=2"},
+    "dw15_nolookback": {"WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK"},
+    "dw15_nostore": {"WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_STORE"},
 }
 if len(sys.argv) > 3:
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in sys.argv[3].split(",")}
 KNOBS = ("WARPDB_COMPACT_SCHED", "WARPDB_COMPACT_GROUPS", "WARPDB_COMPACT_BPC", "WARPDB_EXTRA_DEFINES",
-         "WARPDB_COMPACT_BPC_FORCE")
+         "WARPDB_COMPACT_BPC_FORCE", "WARPDB_COMPACT_DWAVES")
 
 
 def setenv(v):

@@ -28,12 +28,13 @@ typedef unsigned int wx_u32;
 #ifndef WX_COMPACT_GROUPS
 #define WX_COMPACT_GROUPS 4  // row quads per thread per tile (host passes its choice)
 #endif
-#define WX_COMPACT_TILE (WX_BLOCK * 4 * WX_COMPACT_GROUPS)
+#ifndef WX_COMPACT_DWAVES
+#define WX_COMPACT_DWAVES 15  // data waves per compaction workgroup (host passes its choice)
+#endif
 #define WX_GROUP_WINDOW 2048
 #define WX_GROUP_HSORT_MAX 4096
 #define WX_TOPK_MAX 32
 #define WX_SORT_LDS (WX_BLOCK * 8)
-#define WX_COMPACT_CBLOCK (WX_BLOCK + 64)  // 4 data waves + 1 control wave
 
 struct WxDenseArgs {
   const void *col[WX_MAX_COLS];

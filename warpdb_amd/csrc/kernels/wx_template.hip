@@ -163,27 +163,30 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 #if WX_OP == WX_OP_COMPACT
 // Ordered stream compaction in one pass: decoupled look-back over tiles.
 //
-// Tile = 256 data threads x WX_GROUPS groups x 4 rows; row (g, thread, e)
-// of a tile is at offset g*1024 + thread*4 + e, so each group is one 16-byte
+// Tile = WX_DTHREADS data threads x WX_GROUPS groups x 4 rows; row
+// (g, thread, e) of a tile is at offset g*4*WX_DTHREADS + thread*4 + e, so each group is one 16-byte
 // load per lane per column.  In-tile ranks come from 64-bit wavefront ballots
-// (v_mbcnt) and a 4-wave x WX_GROUPS LDS table.  A tile's global offset comes
+// (v_mbcnt) and a WX_DWAVES x WX_GROUPS LDS table.  A tile's global offset comes
 // from its predecessors' 8-byte status words {flag:2 | value:62}; a status
 // word is its own payload (single agent-scope 8-byte stores and loads), so no
 // fence is needed, and output rows are never read inside the launch.
 //
 // wx_project_compact (default) is a persistent, software-pipelined kernel:
-// 4 data waves + 1 control wave per workgroup.  Iteration k: the data waves
-// evaluate tile t_k (its loads were issued one iteration earlier), rank the
-// passing rows, stage (value, tile-local row) in LDS and issue the loads of
-// t_{k+1}; the control wave publishes t_k's aggregate and runs its look-back
-// while the data waves store t_{k-1} from LDS (coalesced) and evaluate
-// t_{k+1}.  Block b owns tiles b, b + grid, ... so the grid must be
+// WX_DWAVES data waves + 1 control wave per workgroup, one LDS stage buffer.
+// Iteration k: the data waves evaluate tile t_k (loaded one iteration
+// earlier), issue t_{k+1}'s loads and rank t_k; the control wave publishes
+// t_k's aggregate while the data waves write t_{k-1} out of LDS (coalesced,
+// its offset resolved one iteration earlier); then the data waves stage
+// (value, tile-local row) of t_k into LDS and evaluate t_{k+1} while the
+// control wave runs t_k's look-back.  Block b owns tiles b, b + grid, ... so the grid must be
 // co-resident (the host sizes it from the occupancy query).
 // wx_project_compact_ticket takes one tile per workgroup from a ticket
 // counter: no residency assumption, no pipelining.
 #define WX_GROUPS WX_COMPACT_GROUPS
-#define WX_TILE WX_COMPACT_TILE
-#define WX_CBLOCK (WX_BLOCK + 64)
+#define WX_DWAVES WX_COMPACT_DWAVES             // data waves per workgroup
+#define WX_DTHREADS (WX_DWAVES * 64)
+#define WX_TILE (WX_DTHREADS * 4 * WX_GROUPS)  // rows per tile
+#define WX_CBLOCK (WX_DTHREADS + 64)            // + 1 control wave
 #define WX_FLAG_A (1ull << 62)
 #define WX_FLAG_P (2ull << 62)
 #define WX_VAL_MASK ((1ull << 62) - 1ull)
@@ -200,7 +203,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 // Per-column input registers of one tile and the load/bind helpers.
 #define WX_DECL_TILE_IN(name, T, slot) T wx_in##slot[WX_GROUPS][4];
 #define WX_LOAD_TILE_IN(name, T, slot) \
-  ::wx::load4<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)wx_dt * 4, wx_a.n_rows, wx_in##slot[wx_g]);
+  ::wx::load4<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4, wx_a.n_rows, wx_in##slot[wx_g]);
 #define WX_BIND_TILE_IN(name, T, slot) const ::wx::reg<T> name{wx_in##slot[wx_g][wx_e]};
 
 // Exclusive prefix of `tile` from its predecessors' status words; one wave.
@@ -271,7 +274,7 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
   _Pragma("unroll") for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {                                     \
     _Pragma("unroll") for (int wx_e = 0; wx_e < 4; ++wx_e) {                                           \
       WX_COLS(WX_BIND_TILE_IN)                                                                           \
-      const wx_i64 idx = tile_base + (wx_i64)wx_g * (WX_BLOCK * 4) + (wx_i64)wx_dt * 4 + wx_e;          \
+      const wx_i64 idx = tile_base + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4 + wx_e;          \
       bool wx_k = idx < wx_a.n_rows;                                                                     \
       wx_k = wx_k && WX_EVAL_COND();                                                                     \
       wx_keep[wx_g][wx_e] = wx_k;                                                                        \
@@ -292,7 +295,7 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
 #define WX_BASES(S_CNT)                                        \
   _Pragma("unroll") for (int g = 0; g < WX_GROUPS; ++g) {    \
     wx_u32 before = 0, gsum = 0;                               \
-    _Pragma("unroll") for (int w = 0; w < WX_WAVES; ++w) {   \
+    _Pragma("unroll") for (int w = 0; w < WX_DWAVES; ++w) {   \
       const wx_u32 c = S_CNT[w][g];                            \
       before += (w < wave) ? c : 0u;                           \
       gsum += c;                                               \
@@ -302,12 +305,12 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
   }
 
 extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCompactArgs wx_a) {
-  __shared__ wx_u32 s_cnt[2][WX_WAVES][WX_GROUPS];
-  __shared__ float s_val[2][WX_TILE];
-  __shared__ unsigned short s_off[2][WX_TILE];
-  __shared__ wx_i64 s_excl[2];
+  __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
+  __shared__ float s_val[WX_TILE];
+  __shared__ unsigned short s_off[WX_TILE];
+  __shared__ wx_i64 s_excl;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool control = wave == WX_WAVES;
+  const bool control = wave == WX_DWAVES;
   const int wx_dt = tid;  // data-thread index (data waves only)
   const wx_i64 grid = gridDim.x;
   wx_i64 tile = blockIdx.x;
@@ -322,32 +325,22 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
     const bool have = tile < wx_a.n_tiles;
     const bool have_prev = k > 0 && tile - grid < wx_a.n_tiles;
     if (!have && !have_prev) break;
-    const int buf = k & 1;
     const wx_i64 tile_base = tile * WX_TILE;
     bool wx_keep[WX_GROUPS][4];
     float wx_val[WX_GROUPS][4];
     wx_u32 lane_pre[WX_GROUPS];
-    // phase 1: evaluate + rank t_k (data waves)
-    if (!control && have) { WX_EVAL_AND_RANK(s_cnt[buf]) }
-    __syncthreads();
-    // phase 2: control publishes t_k's aggregate; data waves stage t_k and prefetch t_{k+1}
-    wx_u32 block_total = 0;
-    wx_u32 grp_base[WX_GROUPS];
-    if (have) { WX_BASES(s_cnt[buf]) }
-    if (control) {
-      if (have && lane == 0)
-        wx::st_agent(&wx_a.status[tile], (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
-    } else if (have) {
+    // phase 1 (data): evaluate t_k, issue t_{k+1}'s loads, rank t_k
+    if (!control && have) {
 #pragma unroll
-      for (int g = 0; g < WX_GROUPS; ++g) {
-        wx_u32 pos = grp_base[g] + lane_pre[g];
+      for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if (wx_keep[g][e]) {
-            s_val[buf][pos] = wx_val[g][e];
-            s_off[buf][pos] = (unsigned short)(g * (WX_BLOCK * 4) + wx_dt * 4 + e);
-            ++pos;
-          }
+        for (int wx_e = 0; wx_e < 4; ++wx_e) {
+          WX_COLS(WX_BIND_TILE_IN)
+          const wx_i64 idx = tile_base + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4 + wx_e;
+          bool wx_k = idx < wx_a.n_rows;
+          wx_k = wx_k && WX_EVAL_COND();
+          wx_keep[wx_g][wx_e] = wx_k;
+          wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
         }
       }
       const wx_i64 next = tile + grid;
@@ -356,9 +349,47 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
 #pragma unroll
         for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
       }
+#pragma unroll
+      for (int g = 0; g < WX_GROUPS; ++g) {
+        wx_u32 pre = 0, tot = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const wx_u64 m = __builtin_amdgcn_ballot_w64(wx_keep[g][e]);
+          pre += wx::lanes_below(m);
+          tot += (wx_u32)__builtin_popcountll(m);
+        }
+        lane_pre[g] = pre;
+        if (lane == 0) s_cnt[wave][g] = tot;
+      }
     }
     __syncthreads();
-    // phase 3: control resolves t_k's offset; data waves write out t_{k-1}
+    // phase 2: control publishes t_k's aggregate; data waves write t_{k-1} out of LDS
+    wx_u32 block_total = 0;
+    wx_u32 grp_base[WX_GROUPS];
+    if (have) { WX_BASES(s_cnt) }
+    if (control) {
+      if (have && lane == 0)
+        wx::st_agent(&wx_a.status[tile], (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
+    } else if (have_prev) {
+      const wx_i64 excl = s_excl;
+      const wx_i64 prev_base = wx_a.row_base + (tile - grid) * WX_TILE;
+#if !WX_DIAG_NO_STORE
+      for (int i = wx_dt; i < (int)prev_total; i += WX_DTHREADS) {
+        const wx_i64 pos = excl + i;
+        if (wx_a.out_val) wx_a.out_val[pos] = s_val[i];
+        if (wx_a.out_idx) {
+          const wx_i64 gi = prev_base + s_off[i];
+          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
+          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
+        }
+      }
+#else
+      if (excl == -1 && wx_a.out_val) wx_a.out_val[0] = s_val[wx_dt];
+#endif
+    }
+    __syncthreads();
+    // phase 3: data waves stage t_k; the control wave resolves t_k's offset
+    // (overlapping the staging and phase 1 of the next iteration)
     if (control) {
       if (have) {
         wx_i64 excl = 0;
@@ -371,27 +402,23 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
         }
 #endif
         if (lane == 0) {
-          s_excl[buf] = excl;
+          s_excl = excl;
           if (tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
         }
       }
-    } else if (have_prev) {
-      const int pb = buf ^ 1;
-      const wx_i64 excl = s_excl[pb];
-      const wx_i64 prev_base = wx_a.row_base + (tile - grid) * WX_TILE;
-#if !WX_DIAG_NO_STORE
-      for (int i = wx_dt; i < (int)prev_total; i += WX_BLOCK) {
-        const wx_i64 pos = excl + i;
-        if (wx_a.out_val) wx_a.out_val[pos] = s_val[pb][i];
-        if (wx_a.out_idx) {
-          const wx_i64 gi = prev_base + s_off[pb][i];
-          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
-          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
+    } else if (have) {
+#pragma unroll
+      for (int g = 0; g < WX_GROUPS; ++g) {
+        wx_u32 pos = grp_base[g] + lane_pre[g];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if (wx_keep[g][e]) {
+            s_val[pos] = wx_val[g][e];
+            s_off[pos] = (unsigned short)(g * (WX_DTHREADS * 4) + wx_dt * 4 + e);
+            ++pos;
+          }
         }
       }
-#else
-      if (excl == -1 && wx_a.out_val) wx_a.out_val[0] = s_val[pb][wx_dt];
-#endif
     }
     prev_total = block_total;
     tile += grid;
@@ -399,8 +426,8 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
 }
 
 // One tile per workgroup, taken from a ticket counter (robust fallback).
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_compact_ticket(WxCompactArgs wx_a) {
-  __shared__ wx_u32 s_cnt[WX_WAVES][WX_GROUPS];
+extern "C" __global__ __launch_bounds__(WX_DTHREADS) void wx_project_compact_ticket(WxCompactArgs wx_a) {
+  __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
   __shared__ wx_i64 s_excl;
   __shared__ wx_u32 s_tile;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -439,7 +466,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_compact_ticket
   const wx_i64 excl = s_excl;
 #pragma unroll
   for (int g = 0; g < WX_GROUPS; ++g) {
-    const wx_i64 r0 = tile_base + (wx_i64)g * (WX_BLOCK * 4) + (wx_i64)tid * 4;
+    const wx_i64 r0 = tile_base + (wx_i64)g * (WX_DTHREADS * 4) + (wx_i64)tid * 4;
     wx_i64 pos = excl + grp_base[g] + lane_pre[g];
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
