@@ -65,6 +65,30 @@ __device__ __forceinline__ void load4(const void *base, wx_i64 r0, wx_i64 n, T (
   }
 }
 
+// Four rows known to be in range and 16-byte aligned: 16-byte loads only.
+template <typename T>
+__device__ __forceinline__ void load4_full(const void *base, wx_i64 r0, T (&o)[4]) {
+  const T *p = static_cast<const T *>(base);
+  if constexpr (sizeof(T) == 4) {
+    typedef T v4 __attribute__((ext_vector_type(4)));
+    const v4 x = *reinterpret_cast<const v4 *>(p + r0);
+    o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
+  } else {
+    typedef T v2 __attribute__((ext_vector_type(2)));
+    const v2 x = *reinterpret_cast<const v2 *>(p + r0);
+    const v2 y = *reinterpret_cast<const v2 *>(p + r0 + 2);
+    o[0] = x.x; o[1] = x.y; o[2] = y.x; o[3] = y.y;
+  }
+}
+
+// Guarded scalar loads (ragged tail or unaligned columns); zero past the end.
+template <typename T>
+__device__ __forceinline__ void load4_tail(const void *base, wx_i64 r0, wx_i64 n, T (&o)[4]) {
+  const T *p = static_cast<const T *>(base);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) o[e] = (r0 + e < n) ? p[r0 + e] : T(0);
+}
+
 __device__ __forceinline__ wx_u64 ld_agent(const wx_u64 *p) {
   return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -114,6 +138,50 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
   ::wx::load4<T>(wx_a.col[slot], wx_r0, wx_a.n_rows, wx_v##slot);
 #define WX_BIND_REG(name, T, slot) const ::wx::reg<T> name{wx_v##slot[wx_e]};
 #define WX_BIND_PTR(name, T, slot) const T *__restrict__ name = static_cast<const T *>(wx_a.col[slot]);
+
+// Grid-stride kernels: WX_UNROLL row quads per thread per iteration, all
+// loads issued before any evaluation (a data-dependent branch in the
+// evaluation would otherwise stop the compiler from batching them).
+#ifndef WX_STRIDE_SIMPLE
+#define WX_STRIDE_SIMPLE 0  // diagnostic: guarded loads only
+#endif
+#define WX_DECL_U(name, T, slot) T wx_u##slot[WX_UNROLL][4];
+#define WX_LOAD_U_FAST(name, T, slot) ::wx::load4_full<T>(wx_a.col[slot], wx_r0u, wx_u##slot[wx_u]);
+#define WX_LOAD_U(name, T, slot) ::wx::load4_tail<T>(wx_a.col[slot], wx_r0u, wx_a.n_rows, wx_u##slot[wx_u]);
+#define WX_BIND_U(name, T, slot) const ::wx::reg<T> name{wx_u##slot[wx_u][wx_e]};
+// When every quad of the workgroup's batch is complete (a workgroup-uniform
+// test) the loads are unconditional 16-byte loads; only the tail batch takes
+// the guarded path.
+#define WX_STRIDE_LOOP_BEGIN                                                                             \
+  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;                                                           \
+  const wx_i64 wx_nfull = wx_a.n_rows >> 2;                                                              \
+  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;                                                 \
+  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq;                        \
+       wx_q0 += wx_stride * WX_UNROLL) {                                                                 \
+    WX_COLS(WX_DECL_U)                                                                                   \
+    const wx_i64 wx_qlast = wx_q0 - threadIdx.x + (WX_BLOCK - 1) + (WX_UNROLL - 1) * wx_stride;         \
+    if (WX_ALIGNED16 && !WX_STRIDE_SIMPLE && wx_qlast < wx_nfull) {                                      \
+      _Pragma("unroll") for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {                                  \
+        const wx_i64 wx_r0u = (wx_q0 + wx_u * wx_stride) << 2;                                           \
+        WX_COLS(WX_LOAD_U_FAST)                                                                          \
+      }                                                                                                  \
+    } else {                                                                                             \
+      _Pragma("unroll") for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {                                  \
+        const wx_i64 wx_r0u = (wx_q0 + wx_u * wx_stride) << 2;                                           \
+        WX_COLS(WX_LOAD_U)                                                                               \
+      }                                                                                                  \
+    }                                                                                                    \
+    _Pragma("unroll") for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {                                    \
+      const wx_i64 wx_r0 = (wx_q0 + wx_u * wx_stride) << 2;                                              \
+      if (wx_q0 + wx_u * wx_stride < wx_nq) {                                                            \
+        _Pragma("unroll") for (int wx_e = 0; wx_e < 4; ++wx_e) {                                        \
+          WX_COLS(WX_BIND_U)                                                                             \
+          const wx_i64 idx = wx_r0 + wx_e;
+#define WX_STRIDE_LOOP_END \
+  }                        \
+  }                        \
+  }                        \
+  }
 
 #if WX_HAS_COND
 #define WX_EVAL_COND() static_cast<bool>(WX_COND)
@@ -498,27 +566,12 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_reduce_sum(WxSumArgs w
   __shared__ wx_i64 s_cnt[WX_WAVES];
   double wx_acc = 0.0;
   wx_i64 wx_cnt = 0;
-  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
-  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
-  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq; wx_q0 += wx_stride * WX_UNROLL) {
-#pragma unroll
-    for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
-      const wx_i64 wx_q = wx_q0 + wx_u * wx_stride;
-      if (wx_q < wx_nq) {
-        const wx_i64 wx_r0 = wx_q << 2;
-        WX_COLS(WX_DECL_LOAD)
-#pragma unroll
-        for (int wx_e = 0; wx_e < 4; ++wx_e) {
-          WX_COLS(WX_BIND_REG)
-          const wx_i64 idx = wx_r0 + wx_e;
-          const bool wx_k = idx < wx_a.n_rows && WX_EVAL_COND();
-          const float wx_val = static_cast<float>(WX_EXPR);
-          wx_acc += wx_k ? (double)wx_val : 0.0;
-          wx_cnt += wx_k ? 1 : 0;
-        }
-      }
-    }
-  }
+  WX_STRIDE_LOOP_BEGIN
+  const bool wx_k = idx < wx_a.n_rows && WX_EVAL_COND();
+  const float wx_val = static_cast<float>(WX_EXPR);
+  wx_acc += wx_k ? (double)wx_val : 0.0;
+  wx_cnt += wx_k ? 1 : 0;
+  WX_STRIDE_LOOP_END
   double acc = wx::wave_sum_f64(wx_acc);
   wx_i64 cnt = (wx_i64)wx::wave_sum_u64((wx_u64)wx_cnt);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -599,34 +652,19 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs 
   __shared__ wx_u32 wx_s_cnt[WX_GWIN];
   for (int i = threadIdx.x; i < WX_GWIN; i += WX_BLOCK) { wx_s_sum[i] = 0.0; wx_s_cnt[i] = 0u; }
   __syncthreads();
-  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
-  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
-  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq; wx_q0 += wx_stride * WX_UNROLL) {
-#pragma unroll
-    for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
-      const wx_i64 wx_q = wx_q0 + wx_u * wx_stride;
-      if (wx_q < wx_nq) {
-        const wx_i64 wx_r0 = wx_q << 2;
-        WX_COLS(WX_DECL_LOAD)
-#pragma unroll
-        for (int wx_e = 0; wx_e < 4; ++wx_e) {
-          WX_COLS(WX_BIND_REG)
-          const wx_i64 idx = wx_r0 + wx_e;
-          if (idx < wx_a.n_rows && WX_EVAL_COND()) {
-            const int wx_key = static_cast<int>(WX_KEY);
-            const float wx_val = static_cast<float>(WX_EXPR);
-            const wx_u32 wx_bin = (wx_u32)(wx_key - wx_a.key_lo);
-            if (wx_bin < (wx_u32)WX_GWIN) {
-              atomicAdd(&wx_s_sum[wx_bin], (double)wx_val);
-              atomicAdd(&wx_s_cnt[wx_bin], 1u);
-            } else {
-              wx_hash_add(wx_a, wx_key, (double)wx_val);
-            }
-          }
-        }
-      }
+  WX_STRIDE_LOOP_BEGIN
+  if (idx < wx_a.n_rows && WX_EVAL_COND()) {
+    const int wx_key = static_cast<int>(WX_KEY);
+    const float wx_val = static_cast<float>(WX_EXPR);
+    const wx_u32 wx_bin = (wx_u32)(wx_key - wx_a.key_lo);
+    if (wx_bin < (wx_u32)WX_GWIN) {
+      atomicAdd(&wx_s_sum[wx_bin], (double)wx_val);
+      atomicAdd(&wx_s_cnt[wx_bin], 1u);
+    } else {
+      wx_hash_add(wx_a, wx_key, (double)wx_val);
     }
   }
+  WX_STRIDE_LOOP_END
   __syncthreads();
   for (int i = threadIdx.x; i < WX_GWIN; i += WX_BLOCK) {
     const wx_u32 c = wx_s_cnt[i];
@@ -769,9 +807,25 @@ __device__ __forceinline__ bool better(wx_u32 ka, wx_i64 ia, wx_u32 kb, wx_i64 i
 struct TopList {
   wx_u32 k[WX_TOPK_K];
   wx_i64 i[WX_TOPK_K];
+  bool full;  // K real rows held
+  float wf;   // the worst held key as a float (valid when full)
   __device__ __forceinline__ void init() {
 #pragma unroll
     for (int j = 0; j < WX_TOPK_K; ++j) { k[j] = 0u; i[j] = WX_IDX_NONE; }
+    full = false;
+    wf = 0.0f;
+  }
+  // Streaming insert of a row whose index exceeds every held index (rows of a
+  // thread arrive in increasing order): a tie with the worst key never
+  // enters, so one float compare rejects almost every row.
+  __device__ __forceinline__ void offer(float f, wx_i64 idx) {
+    if (full) {
+      const bool in = WX_TOPK_DESC ? (f > wf) : (f < wf);
+      if (!in && !(wf != wf && f == f)) return;  // a NaN worst is beaten by any number
+    }
+    push(rank_of(f), idx);
+    full = i[WX_TOPK_K - 1] != WX_IDX_NONE;
+    wf = key_of(k[WX_TOPK_K - 1]);
   }
   __device__ __forceinline__ void push(wx_u32 key, wx_i64 idx) {
     if (!better(key, idx, k[WX_TOPK_K - 1], i[WX_TOPK_K - 1])) return;
@@ -849,24 +903,9 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
   __shared__ wx_i64 s_i[WX_WAVES][WX_TOPK_K];
   wx::TopList wx_L;
   wx_L.init();
-  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
-  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
-  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq; wx_q0 += wx_stride * WX_UNROLL) {
-#pragma unroll
-    for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
-      const wx_i64 wx_q = wx_q0 + wx_u * wx_stride;
-      if (wx_q < wx_nq) {
-        const wx_i64 wx_r0 = wx_q << 2;
-        WX_COLS(WX_DECL_LOAD)
-#pragma unroll
-        for (int wx_e = 0; wx_e < 4; ++wx_e) {
-          WX_COLS(WX_BIND_REG)
-          const wx_i64 idx = wx_r0 + wx_e;
-          if (idx < wx_a.n_rows && WX_EVAL_COND()) wx_L.push(wx::rank_of(static_cast<float>(WX_EXPR)), idx);
-        }
-      }
-    }
-  }
+  WX_STRIDE_LOOP_BEGIN
+  if (idx < wx_a.n_rows && WX_EVAL_COND()) wx_L.offer(static_cast<float>(WX_EXPR), idx);
+  WX_STRIDE_LOOP_END
   wx_u32 bk[WX_TOPK_K];
   wx_i64 bi[WX_TOPK_K];
   wx::block_merge(wx_L, s_k, s_i, bk, bi);
