@@ -333,6 +333,28 @@ def test_topk_ties_and_filter():
     assert np.array_equal(keys[:m].cpu().numpy(), rk)
 
 
+@pytest.mark.parametrize("desc", [True, False])
+@pytest.mark.parametrize("k", [1, 5, 32])
+def test_topk_heavy_ties_nan_signed_zero(k, desc):
+    # few distinct keys (every key tied thousands of times), NaNs and -0.0/+0.0,
+    # ragged row count: the wave threshold must keep the smallest row indices
+    n = 4_000_037
+    u = synth.uniform_f32(n, 9, 0.0, 1.0)
+    p = np.floor(synth.uniform_f32(n, 1, -3.0, 3.0)).astype(np.float32)
+    p[u < 0.01] = np.nan
+    p[(u >= 0.01) & (u < 0.3)] = np.float32(-0.0)
+    cols = {"price": p, "quantity": synth.uniform_int(n, 2, 1, 100).astype(np.float32)}
+    table, _ = dev_table(cols)
+    keys = torch.empty(k, device="cuda")
+    idx = torch.empty(k, dtype=torch.int64, device="cuda")
+    for cond, ocond in ((None, None), ("(quantity[idx] > 50.0f)", "quantity > 50")):
+        m = wx.topk(table, "price[idx]", cond, None, k, desc, launch(), keys.data_ptr(), idx.data_ptr())
+        rk, ri, _ = ora.topk(ora.HostTable(cols), "price", k, desc, cond=ocond)
+        assert m == len(rk)
+        assert np.array_equal(idx[:m].cpu().numpy(), ri)
+        assert np.array_equal(bits(keys[:m].cpu().numpy()), bits(rk))
+
+
 def test_topk_fewer_rows_than_k():
     cols = read_csv(os.path.join(GOLDEN, "test.csv"))
     table, _ = dev_table(cols)

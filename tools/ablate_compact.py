@@ -39,6 +39,10 @@ VARIANTS = {
     "dw15_g4_lb2": {"WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=2"},
     "dw15_nolookback": {"WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK"},
     "dw15_nostore": {"WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_STORE"},
+    "dw15_plainld": {"WARPDB_EXTRA_DEFINES": "WX_NT_LOAD=0"},
+    "dw15_ntst": {"WARPDB_EXTRA_DEFINES": "WX_NT_STORE=1"},
+    "dw15_plainld_ntst": {"WARPDB_EXTRA_DEFINES": "WX_NT_LOAD=0,WX_NT_STORE=1"},
+    "dw12_ntst": {"WARPDB_COMPACT_DWAVES": "12", "WARPDB_EXTRA_DEFINES": "WX_NT_STORE=1"},
 }
 if len(sys.argv) > 3:
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in sys.argv[3].split(",")}

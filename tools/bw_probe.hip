@@ -1,0 +1,150 @@
+// HBM ceiling probe for the streaming shapes the engine's kernels have:
+//   read2   : read two 4-byte columns (the SUM / top-K / GROUP BY input side)
+//   copy    : read one column, write one column
+//   r2w     : read two columns, write 8 B for 5 of every 8 rows into a dense
+//             output (the compaction's traffic mix without the scan)
+// Variants: workgroups per CU, 16-byte loads in flight per lane, nontemporal.
+// Build: hipcc --offload-arch=gfx950 -O3 -o tools/bw_probe tools/bw_probe.hip
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <algorithm>
+
+typedef float v4f __attribute__((ext_vector_type(4)));
+typedef unsigned v4u __attribute__((ext_vector_type(4)));
+#define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); exit(1); } } while (0)
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read2(const v4f *__restrict__ a, const v4f *__restrict__ b, size_t nq,
+                                             float *out) {
+  float acc = 0.f;
+  size_t stride = (size_t)gridDim.x * 256;
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < nq; i += U * stride) {
+    v4f va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NT) {
+        va[u] = __builtin_nontemporal_load(a + i + u * stride);
+        vb[u] = __builtin_nontemporal_load(b + i + u * stride);
+      } else {
+        va[u] = a[i + u * stride];
+        vb[u] = b[i + u * stride];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += va[u].x * vb[u].x + va[u].y * vb[u].y + va[u].z * vb[u].z + va[u].w * vb[u].w;
+  }
+  for (; i < nq; i += stride) acc += a[i].x * b[i].y;
+  if (acc == 1234.5f) out[0] = acc;
+}
+
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void copy1(const v4f *__restrict__ a, v4f *__restrict__ o, size_t nq) {
+  size_t stride = (size_t)gridDim.x * 256;
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < nq; i += U * stride) {
+    v4f v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(a + i + u * stride) : a[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NT) __builtin_nontemporal_store(v[u], o + i + u * stride);
+      else o[i + u * stride] = v[u];
+    }
+  }
+  for (; i < nq; i += stride) o[i] = a[i];
+}
+
+// reads 2 x 16 B per lane per step; writes 2 x 10 B-equivalent: out vals and
+// idx arrays each receive 5/8 of the input rows' worth of bytes, written as
+// contiguous v4f/v4u so the write volume matches compaction (5 GB per 1B rows)
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void r2w(const v4f *__restrict__ a, const v4f *__restrict__ b,
+                                           v4f *__restrict__ ov, v4u *__restrict__ oi, size_t nq) {
+  size_t stride = (size_t)gridDim.x * 256;
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < nq; i += U * stride) {
+    v4f va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      va[u] = NT ? __builtin_nontemporal_load(a + i + u * stride) : a[i + u * stride];
+      vb[u] = NT ? __builtin_nontemporal_load(b + i + u * stride) : b[i + u * stride];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      size_t j = i + u * stride;
+      // 5 of 8 quads store (j % 8 < 5), output position j*5/8 (dense)
+      if ((j & 7) < 5) {
+        size_t p = (j >> 3) * 5 + (j & 7);
+        v4f r = va[u] * vb[u];
+        v4u ix = (v4u){(unsigned)j * 4, (unsigned)j * 4 + 1, (unsigned)j * 4 + 2, (unsigned)j * 4 + 3};
+        if (NT) {
+          __builtin_nontemporal_store(r, ov + p);
+          __builtin_nontemporal_store(ix, oi + p);
+        } else {
+          ov[p] = r;
+          oi[p] = ix;
+        }
+      }
+    }
+  }
+}
+
+template <typename F>
+float time_it(F f, int reps) {
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  f();
+  CK(hipDeviceSynchronize());
+  std::vector<float> ts;
+  for (int r = 0; r < reps; ++r) {
+    CK(hipEventRecord(e0));
+    f();
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    ts.push_back(ms);
+  }
+  std::sort(ts.begin(), ts.end());
+  return ts[ts.size() / 2];
+}
+
+int main(int argc, char **argv) {
+  size_t n = argc > 1 ? (size_t)atof(argv[1]) : 1000000000ull;
+  size_t nq = n / 4;
+  float *a, *b, *ov, *out;
+  unsigned *oi;
+  CK(hipMalloc(&a, n * 4));
+  CK(hipMalloc(&b, n * 4));
+  CK(hipMalloc(&ov, n * 4));
+  CK(hipMalloc(&oi, n * 4));
+  CK(hipMalloc(&out, 64));
+  CK(hipMemset(a, 0, n * 4));
+  CK(hipMemset(b, 0, n * 4));
+  int cus = 256;
+  hipDeviceProp_t pr;
+  CK(hipGetDeviceProperties(&pr, 0));
+  cus = pr.multiProcessorCount;
+  const int reps = 15;
+  int wpcs[] = {2, 4, 8, 16};
+#define RUN(name, KER, bytes, ...)                                                                            \
+  for (int w : wpcs) {                                                                                        \
+    int g = cus * w;                                                                                          \
+    float ms = time_it([&] { KER<<<g, 256>>>(__VA_ARGS__); }, reps);                                          \
+    printf("%-28s wg/CU %2d  %7.3f ms  %7.1f GB/s\n", name, w, ms, (double)(bytes) / ms / 1e6);               \
+  }
+  RUN("read2 u4", (read2<4, false>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
+  RUN("read2 u8", (read2<8, false>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
+  RUN("read2 u4 nt", (read2<4, true>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
+  RUN("read2 u8 nt", (read2<8, true>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
+  RUN("copy u4", (copy1<4, false>), n * 8, (const v4f *)a, (v4f *)ov, nq);
+  RUN("copy u4 nt", (copy1<4, true>), n * 8, (const v4f *)a, (v4f *)ov, nq);
+  RUN("r2w u4", (r2w<4, false>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+  RUN("r2w u4 nt", (r2w<4, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+  RUN("r2w u8 nt", (r2w<8, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+  return 0;
+}

@@ -42,6 +42,32 @@ struct reg {
   __device__ __forceinline__ operator T() const { return v; }
 };
 
+// Streamed table columns are read once: nontemporal loads (measured +10 %
+// read bandwidth on gfx950, tools/bw_probe.hip).  Results are written once
+// and consumed by a later launch or the host: nontemporal stores optional.
+#ifndef WX_NT_LOAD
+#define WX_NT_LOAD 1
+#endif
+#ifndef WX_NT_STORE
+#define WX_NT_STORE 0
+#endif
+template <typename V>
+__device__ __forceinline__ V ldv(const V *p) {
+#if WX_NT_LOAD
+  return __builtin_nontemporal_load(p);
+#else
+  return *p;
+#endif
+}
+template <typename V>
+__device__ __forceinline__ void stv(V *p, V v) {
+#if WX_NT_STORE
+  __builtin_nontemporal_store(v, p);
+#else
+  *p = v;
+#endif
+}
+
 // Four consecutive rows [r0, r0+4) of one column into registers.  Full,
 // aligned groups use 16-byte loads (global_load_dwordx4); the ragged tail
 // falls back to guarded scalar loads and zero-fills.
@@ -51,12 +77,12 @@ __device__ __forceinline__ void load4(const void *base, wx_i64 r0, wx_i64 n, T (
   if (WX_ALIGNED16 && r0 + 4 <= n) {
     if constexpr (sizeof(T) == 4) {
       typedef T v4 __attribute__((ext_vector_type(4)));
-      const v4 x = *reinterpret_cast<const v4 *>(p + r0);
+      const v4 x = ldv(reinterpret_cast<const v4 *>(p + r0));
       o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
     } else {
       typedef T v2 __attribute__((ext_vector_type(2)));
-      const v2 x = *reinterpret_cast<const v2 *>(p + r0);
-      const v2 y = *reinterpret_cast<const v2 *>(p + r0 + 2);
+      const v2 x = ldv(reinterpret_cast<const v2 *>(p + r0));
+      const v2 y = ldv(reinterpret_cast<const v2 *>(p + r0 + 2));
       o[0] = x.x; o[1] = x.y; o[2] = y.x; o[3] = y.y;
     }
   } else {
@@ -71,12 +97,12 @@ __device__ __forceinline__ void load4_full(const void *base, wx_i64 r0, T (&o)[4
   const T *p = static_cast<const T *>(base);
   if constexpr (sizeof(T) == 4) {
     typedef T v4 __attribute__((ext_vector_type(4)));
-    const v4 x = *reinterpret_cast<const v4 *>(p + r0);
+    const v4 x = ldv(reinterpret_cast<const v4 *>(p + r0));
     o[0] = x.x; o[1] = x.y; o[2] = x.z; o[3] = x.w;
   } else {
     typedef T v2 __attribute__((ext_vector_type(2)));
-    const v2 x = *reinterpret_cast<const v2 *>(p + r0);
-    const v2 y = *reinterpret_cast<const v2 *>(p + r0 + 2);
+    const v2 x = ldv(reinterpret_cast<const v2 *>(p + r0));
+    const v2 y = ldv(reinterpret_cast<const v2 *>(p + r0 + 2));
     o[0] = x.x; o[1] = x.y; o[2] = y.x; o[3] = y.y;
   }
 }
@@ -138,6 +164,8 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
   ::wx::load4<T>(wx_a.col[slot], wx_r0, wx_a.n_rows, wx_v##slot);
 #define WX_BIND_REG(name, T, slot) const ::wx::reg<T> name{wx_v##slot[wx_e]};
 #define WX_BIND_PTR(name, T, slot) const T *__restrict__ name = static_cast<const T *>(wx_a.col[slot]);
+// one row's values (gathered at `idx`), bound like the streamed registers
+#define WX_BIND_ROW(name, T, slot) const ::wx::reg<T> name{static_cast<const T *>(wx_a.col[slot])[idx]};
 
 // Grid-stride kernels: WX_UNROLL row quads per thread per iteration, all
 // loads issued before any evaluation (a data-dependent branch in the
@@ -181,6 +209,12 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
   }                        \
   }                        \
   }                        \
+  }
+// Closes the per-row loops but leaves the batch loop open: code after it
+// sees the whole batch (wx_q0, wx_stride); the caller closes the batch loop.
+#define WX_STRIDE_BATCH_END \
+  }                         \
+  }                         \
   }
 
 #if WX_HAS_COND
@@ -444,11 +478,11 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
 #if !WX_DIAG_NO_STORE
       for (int i = wx_dt; i < (int)prev_total; i += WX_DTHREADS) {
         const wx_i64 pos = excl + i;
-        if (wx_a.out_val) wx_a.out_val[pos] = s_val[i];
+        if (wx_a.out_val) wx::stv(wx_a.out_val + pos, s_val[i]);
         if (wx_a.out_idx) {
           const wx_i64 gi = prev_base + s_off[i];
-          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
-          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
+          if (wx_a.idx64) wx::stv(static_cast<wx_i64 *>(wx_a.out_idx) + pos, gi);
+          else wx::stv(static_cast<int *>(wx_a.out_idx) + pos, (int)gi);
         }
       }
 #else
@@ -559,7 +593,7 @@ extern "C" __global__ __launch_bounds__(WX_DTHREADS) void wx_project_compact_tic
 // WX_UNROLL row quads in flight per thread; one partial per block, combined
 // in a fixed order by wx_sum_finalize (bitwise reproducible).
 #ifndef WX_UNROLL
-#define WX_UNROLL 4
+#define WX_UNROLL 8  // tools/ablate_stream.py: 8 quads in flight, 8 workgroups per CU
 #endif
 extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_reduce_sum(WxSumArgs wx_a) {
   __shared__ double s_sum[WX_WAVES];
@@ -788,7 +822,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroup
 #define WX_TOPK_DESC 1
 #endif
 #ifndef WX_UNROLL
-#define WX_UNROLL 4
+#define WX_UNROLL 8
 #endif
 #define WX_IDX_NONE 0x7fffffffffffffffll
 
@@ -870,6 +904,7 @@ __device__ __forceinline__ void wave_merge(TopList &L, wx_u32 (&out_k)[WX_TOPK_K
 
 // Merge the wave lists of a block through LDS; every thread of wave 0 returns
 // the block's K best (valid in lane 0).
+template <int NW>
 __device__ __forceinline__ void block_merge(TopList &L, wx_u32 (*s_k)[WX_TOPK_K], wx_i64 (*s_i)[WX_TOPK_K],
                                             wx_u32 (&bk)[WX_TOPK_K], wx_i64 (&bi)[WX_TOPK_K]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -882,12 +917,12 @@ __device__ __forceinline__ void block_merge(TopList &L, wx_u32 (*s_k)[WX_TOPK_K]
   }
   __syncthreads();
   if (wave == 0) {
-    int head[WX_WAVES];
+    int head[NW];
 #pragma unroll
-    for (int w = 0; w < WX_WAVES; ++w) head[w] = 0;
+    for (int w = 0; w < NW; ++w) head[w] = 0;
     for (int r = 0; r < WX_TOPK_K; ++r) {
       int best = 0;
-      for (int w = 1; w < WX_WAVES; ++w)
+      for (int w = 1; w < NW; ++w)
         if (better(s_k[w][head[w]], s_i[w][head[w]], s_k[best][head[best]], s_i[best][head[best]])) best = w;
       bk[r] = s_k[best][head[best]];
       bi[r] = s_i[best][head[best]];
@@ -903,12 +938,84 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
   __shared__ wx_i64 s_i[WX_WAVES][WX_TOPK_K];
   wx::TopList wx_L;
   wx_L.init();
-  WX_STRIDE_LOOP_BEGIN
-  if (idx < wx_a.n_rows && WX_EVAL_COND()) wx_L.offer(static_cast<float>(WX_EXPR), idx);
-  WX_STRIDE_LOOP_END
+  // Batches of WX_UNROLL row quads per thread.  Once the lane's list is full
+  // (and its worst key is a number), a complete batch costs one max/min of its
+  // keys against the worst (rows failing the WHERE count as -inf/+inf; NaN
+  // keys never enter a full list; ties never enter, later rows lose): only
+  // batches that can change the list re-evaluate their rows and insert.
+  const float wx_none = WX_TOPK_DESC ? -__builtin_inff() : __builtin_inff();
+  float wx_T = wx_none;  // wave threshold: best worst-key over the wave's full lanes
+  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
+  const wx_i64 wx_nfull = wx_a.n_rows >> 2;
+  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq; wx_q0 += wx_stride * WX_UNROLL) {
+    WX_COLS(WX_DECL_U)
+    const wx_i64 wx_qlast = wx_q0 - threadIdx.x + (WX_BLOCK - 1) + (WX_UNROLL - 1) * wx_stride;
+    const bool wx_whole = WX_ALIGNED16 && wx_qlast < wx_nfull;  // workgroup-uniform
+    if (wx_whole) {
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+        const wx_i64 wx_r0u = (wx_q0 + wx_u * wx_stride) << 2;
+        WX_COLS(WX_LOAD_U_FAST)
+      }
+    } else {
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+        const wx_i64 wx_r0u = (wx_q0 + wx_u * wx_stride) << 2;
+        WX_COLS(WX_LOAD_U)
+      }
+    }
+    bool wx_slow = !wx_whole || !wx_L.full || wx_L.wf != wx_L.wf;
+    if (!wx_slow) {
+      // wx_T >= this lane's worst: rows strictly worse than T cannot reach the
+      // top K (T is the K-th best of another lane's rows); rows equal to T may
+      // (smaller index), and rows equal to the lane's own worst may not.
+      float wx_m = wx_none;
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e) {
+          WX_COLS(WX_BIND_U)
+          const wx_i64 idx = ((wx_q0 + wx_u * wx_stride) << 2) + wx_e;
+          (void)idx;
+          const float wx_v = WX_EVAL_COND() ? static_cast<float>(WX_EXPR) : wx_none;
+          wx_m = WX_TOPK_DESC ? fmaxf(wx_m, wx_v) : fminf(wx_m, wx_v);
+        }
+      }
+      const bool wx_tie_ok = WX_TOPK_DESC ? (wx_T > wx_L.wf) : (wx_T < wx_L.wf);
+      wx_slow = WX_TOPK_DESC ? (wx_tie_ok ? wx_m >= wx_T : wx_m > wx_L.wf)
+                             : (wx_tie_ok ? wx_m <= wx_T : wx_m < wx_L.wf);
+    }
+    if (wx_slow) {
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+        if (wx_q0 + wx_u * wx_stride < wx_nq) {
+#pragma unroll
+          for (int wx_e = 0; wx_e < 4; ++wx_e) {
+            WX_COLS(WX_BIND_U)
+            const wx_i64 idx = ((wx_q0 + wx_u * wx_stride) << 2) + wx_e;
+            if (idx < wx_a.n_rows && WX_EVAL_COND()) {
+              const float wx_f = static_cast<float>(WX_EXPR);
+              if (!(WX_TOPK_DESC ? wx_f < wx_T : wx_f > wx_T)) wx_L.offer(wx_f, idx);
+            }
+          }
+        }
+      }
+    }
+    // refresh the wave threshold after any insert in the wave
+    if (__builtin_amdgcn_ballot_w64(wx_slow)) {
+      float t = (wx_L.full && wx_L.wf == wx_L.wf) ? wx_L.wf : wx_none;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const float x = __shfl_xor(t, o);
+        t = WX_TOPK_DESC ? fmaxf(t, x) : fminf(t, x);
+      }
+      wx_T = t;
+    }
+  }
   wx_u32 bk[WX_TOPK_K];
   wx_i64 bi[WX_TOPK_K];
-  wx::block_merge(wx_L, s_k, s_i, bk, bi);
+  wx::block_merge<WX_WAVES>(wx_L, s_k, s_i, bk, bi);
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int j = 0; j < WX_TOPK_K; ++j) {
@@ -918,18 +1025,33 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
   }
 }
 
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_finalize(WxTopkFinArgs wx_a) {
-  __shared__ wx_u32 s_k[WX_WAVES][WX_TOPK_K];
-  __shared__ wx_i64 s_i[WX_WAVES][WX_TOPK_K];
+// One 1024-thread block; candidate loads are issued 8 per thread at a time
+// (the loop is latency-bound otherwise: the candidates sit in other XCDs' L2).
+#define WX_FIN_BLOCK 1024
+#define WX_FIN_BATCH 8
+extern "C" __global__ __launch_bounds__(WX_FIN_BLOCK) void wx_topk_finalize(WxTopkFinArgs wx_a) {
+  __shared__ wx_u32 s_k[WX_FIN_BLOCK / 64][WX_TOPK_K];
+  __shared__ wx_i64 s_i[WX_FIN_BLOCK / 64][WX_TOPK_K];
   __shared__ wx_u32 s_bk[WX_TOPK_K];
   __shared__ wx_i64 s_bi[WX_TOPK_K];
   wx::TopList L;
   L.init();
-  for (wx_i64 c = threadIdx.x; c < wx_a.n_cand; c += WX_BLOCK)
-    if (wx_a.cand_i[c] != WX_IDX_NONE) L.push(wx_a.cand_k[c], wx_a.cand_i[c]);
+  for (wx_i64 c0 = threadIdx.x; c0 < wx_a.n_cand; c0 += (wx_i64)WX_FIN_BLOCK * WX_FIN_BATCH) {
+    wx_u32 ck[WX_FIN_BATCH];
+    wx_i64 ci[WX_FIN_BATCH];
+#pragma unroll
+    for (int b = 0; b < WX_FIN_BATCH; ++b) {
+      const wx_i64 c = c0 + (wx_i64)b * WX_FIN_BLOCK;
+      ck[b] = c < wx_a.n_cand ? wx_a.cand_k[c] : 0u;
+      ci[b] = c < wx_a.n_cand ? wx_a.cand_i[c] : WX_IDX_NONE;
+    }
+#pragma unroll
+    for (int b = 0; b < WX_FIN_BATCH; ++b)
+      if (ci[b] != WX_IDX_NONE) L.push(ck[b], ci[b]);
+  }
   wx_u32 bk[WX_TOPK_K];
   wx_i64 bi[WX_TOPK_K];
-  wx::block_merge(L, s_k, s_i, bk, bi);
+  wx::block_merge<WX_FIN_BLOCK / 64>(L, s_k, s_i, bk, bi);
   if (threadIdx.x == 0) {
     int n = 0;
 #pragma unroll
@@ -944,12 +1066,13 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_finalize(WxTopkFi
   const int wx_j = threadIdx.x;
   if (wx_j < WX_TOPK_K && s_bi[wx_j] != WX_IDX_NONE) {
     const wx_i64 idx = s_bi[wx_j];
-    const float wx_key = wx::key_of(s_bk[wx_j]);
+    WX_COLS(WX_BIND_ROW)
+    // the row's own key (not the rank's image: keeps -0.0 and NaN bits)
+    const float wx_key = static_cast<float>(WX_EXPR);
     if (wx_a.out_keys) wx_a.out_keys[wx_j] = wx_key;
     if (wx_a.out_idx) wx_a.out_idx[wx_j] = wx_a.row_base + idx;
     if (wx_a.out_vals) {
 #if WX_HAS_SELECT
-      WX_COLS(WX_BIND_PTR)
       wx_a.out_vals[wx_j] = static_cast<float>(WX_SELECT);
 #else
       wx_a.out_vals[wx_j] = wx_key;
