@@ -17,6 +17,12 @@
  *   wx_topk             jit_sort_float + LIMIT   src/warpdb.cpp:453-455,483-495
  *   wx_reduce_sum       per-shard SUM of query_multi_gpu (new; the reference
  *                       gathers dense results on the host, src/multi_gpu_utils.cpp:5-63)
+ *   wx_reduce_stats     ungrouped SUM / COUNT / AVG / MIN / MAX of query_sql
+ *                       (src/warpdb.cpp:297-498, AggData :383-384) and the column
+ *                       statistics of the optimizer (include/csv_loader.hpp:22-37,
+ *                       src/optimizer.cpp:13-17)
+ *   wx_group_agg        jit_group_sum + the per-group MIN / MAX of query_sql's
+ *                       AggData (src/warpdb.cpp:375-385)
  *
  * Expression inputs are the reference's lowered C expressions over
  * identifiers `<column>[idx]` (include/expression.hpp:32-78), e.g.
@@ -108,16 +114,40 @@ wx_status wx_reduce_sum(const wx_table *table, const char *expr, const char *con
                         const wx_launch *launch, void *d_out, double *h_sum, int64_t *h_count,
                         char *err, size_t errlen);
 
+/* SUM / COUNT / MIN / MAX of (float)expr over rows where cond holds.  MIN and
+ * MAX skip NaN values and read NaN when no value qualifies (SQL NULL); -0.0
+ * and +0.0 compare equal and come back as +0.0. */
+typedef struct wx_stats {
+  double sum;
+  int64_t count;
+  float min;
+  float max;
+} wx_stats;
+
+/* d_out (device, nullable): a wx_stats; h_out (host, nullable) synchronises. */
+wx_status wx_reduce_stats(const wx_table *table, const char *expr, const char *cond,
+                          const wx_launch *launch, void *d_out, wx_stats *h_out, char *err,
+                          size_t errlen);
+
 /* SUM((float)val_expr) GROUP BY (int)key_expr WHERE cond.  Sums in double,
  * counts in int64, groups in ascending key order.  capacity = entries of the
  * device outputs (and the distinct-key bound of the general-key table).
- * Keys in [key_window_lo, key_window_lo + 4096) take the LDS fast path. */
+ * Keys in [key_window_lo, key_window_lo + 2048) take the LDS fast path; at
+ * most 4096 distinct keys may fall outside it. */
 wx_status wx_group_sum(const wx_table *table, const char *val_expr, const char *key_expr,
                        const char *cond, const wx_launch *launch, int32_t key_window_lo,
                        int64_t capacity, int32_t *d_keys, double *d_sums, int64_t *d_counts,
                        int64_t *d_n_groups, int64_t *h_n_groups, char *err, size_t errlen);
 
-/* ORDER BY order_expr [DESC] LIMIT k (1 <= k <= 256) over rows where cond
+/* wx_group_sum plus per-group MIN / MAX of (float)val_expr (d_mins / d_maxs,
+ * nullable, `capacity` entries; NaN skipped as in wx_reduce_stats). */
+wx_status wx_group_agg(const wx_table *table, const char *val_expr, const char *key_expr,
+                       const char *cond, const wx_launch *launch, int32_t key_window_lo,
+                       int64_t capacity, int32_t *d_keys, double *d_sums, int64_t *d_counts,
+                       float *d_mins, float *d_maxs, int64_t *d_n_groups, int64_t *h_n_groups,
+                       char *err, size_t errlen);
+
+/* ORDER BY order_expr [DESC] LIMIT k (1 <= k <= 32) over rows where cond
  * holds; ties broken by ascending row index.  Outputs (device, nullable):
  * order keys, row_base + row indices, and (float)select_expr at those rows
  * (select_expr NULL = the order key).  The count (<= k) goes to d_count / h_count. */
@@ -143,7 +173,8 @@ wx_status wx_fill_synthetic(void *d_ptr, int32_t dtype, int64_t n, uint64_t seed
 
 /* Build (and cache) the kernels a call would use, without launching.  Works
  * without a GPU (arch taken from $WARPDB_ARCH, default gfx950).  op: 0 project
- * dense, 1 project compact, 2 sum, 3 group, 4 topk.  src_out (nullable)
+ * dense, 1 project compact, 2 sum, 3 group, 4 topk (k = LIMIT; for sum and
+ * group, k = 1 selects the MIN / MAX build).  src_out (nullable)
  * receives the generated HIP source. */
 wx_status wx_prepare(const wx_table *table, int32_t op, const char *expr, const char *cond,
                      const char *aux_expr, int32_t k, const wx_launch *launch, char *src_out,

@@ -583,12 +583,53 @@ int ora_sum(const ora_table *t, const char *expr, const char *cond, int sem, dou
   return 0;
 }
 
+/* MIN / MAX fold of the reference's AggData (src/warpdb.cpp:375-385: min/max
+ * of the group's values).  Stated order-free: NaN values are skipped (the
+ * reference's std::min/std::max keep or drop a NaN depending on where it falls
+ * in the scan), -0.0 folds to +0.0, and an empty fold reads NaN. */
+static inline void mm_fold(float v, int *have, float *mn, float *mx) {
+  if (isnan(v)) return;
+  if (v == 0.0f) v = 0.0f;
+  if (!*have) { *mn = *mx = v; *have = 1; return; }
+  if (v < *mn) *mn = v;
+  if (v > *mx) *mx = v;
+}
+
+int ora_stats(const ora_table *t, const char *expr, const char *cond, int sem, double *out_sum,
+              int64_t *out_count, float *out_min, float *out_max, char *err, size_t errlen) {
+  errctx e = {err, errlen, 0};
+  node *ex = prep(expr, t, &e, 0);
+  if (e.failed) return -1;
+  node *cx = prep(cond, t, &e, 1);
+  if (e.failed) { freenode(ex); return -1; }
+  double s = 0.0;
+  int64_t k = 0;
+  int have = 0;
+  float mn = NAN, mx = NAN;
+  for (int64_t i = 0; i < t->n_rows; i++) {
+    if (!eval_cond(cx, t, i, sem)) continue;
+    const float v = eval_val(ex, t, i, sem);
+    s += (double)v;
+    k++;
+    mm_fold(v, &have, &mn, &mx);
+  }
+  if (out_sum) *out_sum = s;
+  if (out_count) *out_count = k;
+  if (out_min) *out_min = mn;
+  if (out_max) *out_max = mx;
+  freenode(ex);
+  freenode(cx);
+  return 0;
+}
+
 /* open-addressing int -> slot map for GROUP BY */
 typedef struct {
   int32_t key;
   int used;
   double sum;
   int64_t cnt;
+  int have_mm;
+  float mn, mx;
 } gslot;
 
 static int cmp_gslot(const void *a, const void *b) {
@@ -596,9 +637,10 @@ static int cmp_gslot(const void *a, const void *b) {
   return (x->key > y->key) - (x->key < y->key);
 }
 
-int ora_group_sum(const ora_table *t, const char *val_expr, const char *key_expr, const char *cond,
+int ora_group_agg(const ora_table *t, const char *val_expr, const char *key_expr, const char *cond,
                   int sem, int64_t capacity, int32_t *out_keys, double *out_sums,
-                  int64_t *out_counts, int64_t *out_groups, char *err, size_t errlen) {
+                  int64_t *out_counts, float *out_mins, float *out_maxs, int64_t *out_groups, char *err,
+                  size_t errlen) {
   errctx e = {err, errlen, 0};
   node *vx = prep(val_expr, t, &e, 0);
   if (e.failed) return -1;
@@ -628,9 +670,10 @@ int ora_group_sum(const ora_table *t, const char *val_expr, const char *key_expr
     }
     size_t h = ((uint32_t)key * 2654435761u) & (cap - 1);
     while (tab[h].used && tab[h].key != key) h = (h + 1) & (cap - 1);
-    if (!tab[h].used) { tab[h].used = 1; tab[h].key = key; used++; }
+    if (!tab[h].used) { tab[h].used = 1; tab[h].key = key; tab[h].mn = tab[h].mx = NAN; used++; }
     tab[h].sum += (double)val;
     tab[h].cnt += 1;
+    mm_fold(val, &tab[h].have_mm, &tab[h].mn, &tab[h].mx);
   }
   /* compact + ascending key order */
   size_t g = 0;
@@ -644,6 +687,8 @@ int ora_group_sum(const ora_table *t, const char *val_expr, const char *key_expr
       if (out_keys) out_keys[s] = tab[s].key;
       if (out_sums) out_sums[s] = tab[s].sum;
       if (out_counts) out_counts[s] = tab[s].cnt;
+      if (out_mins) out_mins[s] = tab[s].mn;
+      if (out_maxs) out_maxs[s] = tab[s].mx;
     }
   }
   *out_groups = (int64_t)g;
@@ -652,6 +697,13 @@ int ora_group_sum(const ora_table *t, const char *val_expr, const char *key_expr
   freenode(kx);
   freenode(cx);
   return e.failed ? -1 : 0;
+}
+
+int ora_group_sum(const ora_table *t, const char *val_expr, const char *key_expr, const char *cond,
+                  int sem, int64_t capacity, int32_t *out_keys, double *out_sums,
+                  int64_t *out_counts, int64_t *out_groups, char *err, size_t errlen) {
+  return ora_group_agg(t, val_expr, key_expr, cond, sem, capacity, out_keys, out_sums, out_counts, NULL, NULL,
+                       out_groups, err, errlen);
 }
 
 /* total order used by top-K: key (desc or asc), then row index ascending.

@@ -72,6 +72,15 @@ int ora_sum(const ora_table *t, const char *expr, const char *cond, int sem,
 /* SUM(val) GROUP BY key WHERE cond.  key = (int)eval(key_expr), val =
  * (float)eval(val_expr), accumulated in double; groups in ascending key
  * order (tests/sql_features_test.cpp:14-19).  Capacity = max groups. */
+/* SUM / COUNT / MIN / MAX of (float)expr WHERE cond; MIN / MAX skip NaN,
+ * fold -0.0 to +0.0 and read NaN when empty (AggData, src/warpdb.cpp:375-385). */
+int ora_stats(const ora_table *t, const char *expr, const char *cond, int sem, double *out_sum,
+              int64_t *out_count, float *out_min, float *out_max, char *err, size_t errlen);
+/* ora_group_sum plus per-group MIN / MAX (nullable outputs). */
+int ora_group_agg(const ora_table *t, const char *val_expr, const char *key_expr, const char *cond,
+                  int sem, int64_t capacity, int32_t *out_keys, double *out_sums,
+                  int64_t *out_counts, float *out_mins, float *out_maxs, int64_t *out_groups, char *err,
+                  size_t errlen);
 int ora_group_sum(const ora_table *t, const char *val_expr, const char *key_expr,
                   const char *cond, int sem, int64_t capacity, int32_t *out_keys,
                   double *out_sums, int64_t *out_counts, int64_t *out_groups, char *err,

@@ -7,11 +7,14 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <iostream>
+#include <sstream>
 #include <functional>
 #include <map>
 #include <vector>
 
 #include "warpdb/jit.hpp"
+#include "warpdb/optimizer.hpp"
 #include "warpdb/warpdb.hpp"
 
 static int failures = 0;
@@ -114,6 +117,27 @@ int main() {
     WarpDB db("tests/golden/test.json");
     auto r = db.query("price * quantity WHERE price > 15");
     CHECK(r.size() == 4 && r[0] == 0.0f && r[1] == 80.0f && r[3] == 150.0f);
+  }
+  // --- optimizer (src/optimizer.cpp): execute_query_optimized output
+  {
+    WarpDB db("tests/golden/test.csv");
+    Table &t = const_cast<Table &>(db.table());
+    std::ostringstream cap;
+    auto *old = std::cout.rdbuf(cap.rdbuf());
+    execute_query_optimized("price * quantity", "price > 100", t);
+    execute_query_optimized("price * 2", "price > 15", t);
+    std::cout.rdbuf(old);
+    CHECK(cap.str() == "[Optimizer] Filter eliminates all rows.\nResult[0] = 0\nResult[1] = 40\n"
+                       "Result[2] = 30.5\nResult[3] = 60\n");
+    bool at = false, af = false;
+    TableStats ts;
+    ts.price.min = 10.5f;
+    ts.price.max = 30.0f;
+    ts.quantity.min = 2;
+    ts.quantity.max = 5;
+    auto cond = parse_expression(tokenize("price > 10 AND quantity < 6"));
+    analyze_condition(cond.get(), ts, at, af);
+    CHECK(at && !af);
   }
   if (failures) return 1;
   std::printf("engine_test: all passed\n");

@@ -46,6 +46,8 @@ def lib():
         _lib.ora_project_filter.argtypes = [T, E, E, I32, P, P, P, P, E, S]
         _lib.ora_sum.argtypes = [T, E, E, I32, P, P, E, S]
         _lib.ora_group_sum.argtypes = [T, E, E, E, I32, I64, P, P, P, P, E, S]
+        _lib.ora_stats.argtypes = [T, E, E, I32, P, P, P, P, E, S]
+        _lib.ora_group_agg.argtypes = [T, E, E, E, I32, I64, P, P, P, P, P, P, E, S]
         _lib.ora_topk.argtypes = [T, E, E, E, I64, I32, I32, P, P, P, P, E, S]
         _lib.ora_scan_baseline.argtypes = [T, E, P, P]
         _lib.ora_scan_baseline.restype = I64
@@ -132,6 +134,33 @@ def group_sum(t: HostTable, val_expr: str, key_expr: str, cond: Optional[str] = 
                              cnts.ctypes.data, ctypes.addressof(g), err, len(err)), err)
     n = g.value
     return keys[:n], sums[:n], cnts[:n]
+
+
+def stats(t: HostTable, expr: str, cond: Optional[str] = None, sem: int = SEM_JIT):
+    s, c = ctypes.c_double(0), ctypes.c_int64(0)
+    mn, mx = ctypes.c_float(0), ctypes.c_float(0)
+    err = _err()
+    _chk(lib().ora_stats(ctypes.byref(t.c), expr.encode(), cond.encode() if cond else None, sem,
+                         ctypes.addressof(s), ctypes.addressof(c), ctypes.addressof(mn), ctypes.addressof(mx),
+                         err, len(err)), err)
+    return s.value, c.value, np.float32(mn.value), np.float32(mx.value)
+
+
+def group_agg(t: HostTable, val_expr: str, key_expr: str, cond: Optional[str] = None, sem: int = SEM_JIT,
+              capacity: int = 1 << 20):
+    keys = np.empty(capacity, np.int32)
+    sums = np.empty(capacity, np.float64)
+    cnts = np.empty(capacity, np.int64)
+    mins = np.empty(capacity, np.float32)
+    maxs = np.empty(capacity, np.float32)
+    g = ctypes.c_int64(0)
+    err = _err()
+    _chk(lib().ora_group_agg(ctypes.byref(t.c), val_expr.encode(), key_expr.encode(),
+                             cond.encode() if cond else None, sem, capacity, keys.ctypes.data, sums.ctypes.data,
+                             cnts.ctypes.data, mins.ctypes.data, maxs.ctypes.data, ctypes.addressof(g), err,
+                             len(err)), err)
+    n = g.value
+    return keys[:n], sums[:n], cnts[:n], mins[:n], maxs[:n]
 
 
 def topk(t: HostTable, order_expr: str, k: int, descending: bool = True, cond: Optional[str] = None,

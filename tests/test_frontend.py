@@ -89,7 +89,59 @@ def test_plan_shards_matches_reference_partition():
     assert len(s) == 8 and s[-1][2] == n and all(e - b == 1_000_000_000 for _, b, e in s)
 
 
-def test_cpp_frontend_binary():
+def test_optimizer_verdicts():
+    # the reference's analyze_condition never decides (src/optimizer.cpp:13-17)
+    st = {"price": (0.0, 39.99, 0, False), "quantity": (1.0, 100.0, 0, True)}
+    cases = {"price > 40": "always_false", "price >= 0": "always_true", "price > 15": "unknown",
+             "price > 10 AND quantity > 200": "always_false", "price > 50 OR quantity >= 1": "always_true",
+             "price * 2 > 80": "always_false", "quantity / quantity > 2": "unknown", "price != 100": "always_true",
+             "discount(price, 0.9) > 1000": "unknown", "missing > 1": "unknown"}
+    for w, v in cases.items():
+        assert pw.analyze_condition(w, st) == v, w
+    # NaN rows fail every comparison but pass !=
+    nan = {"price": (0.0, 39.99, 3, False)}
+    assert pw.analyze_condition("price >= 0", nan) == "unknown"
+    assert pw.analyze_condition("price < 0", nan) == "always_false"
+    assert pw.analyze_condition("price != 100", nan) == "always_true"
+
+
+def test_optimizer_is_sound_against_oracle():
+    # whenever the interval analysis decides, every row must agree (JIT semantics)
+    import numpy as np
+
+    import oracle_lib as ora
+
+    rng = np.random.default_rng(21)
+    atoms = ["a", "b", "k", "1", "2.5", "0.9", "10", "40", "(a + 1)", "(k * 3)", "(a * b)", "(a / 7)", "(k / 3)"]
+    cmps = [">", "<", ">=", "<=", "==", "!="]
+    decided = 0
+    for trial in range(40):
+        n = 400
+        a = rng.uniform(rng.uniform(-50, 0), rng.uniform(0, 50), n).astype(np.float32)
+        b = np.round(rng.uniform(-3, 3, n), 1).astype(np.float32)
+        k = rng.integers(-20, 20, n).astype(np.int32)
+        if trial % 4 == 0:
+            a[rng.uniform(size=n) < 0.1] = np.nan
+        cols = {"a": a, "b": b, "k": k}
+        stats = {}
+        for name, v in cols.items():
+            ok = v[~np.isnan(v)] if v.dtype == np.float32 else v
+            stats[name] = (float(ok.min()), float(ok.max()), int(np.isnan(v).sum()) if v.dtype == np.float32 else 0,
+                           v.dtype == np.int32)
+        t = ora.HostTable(cols)
+        for _ in range(25):
+            def cmp():
+                return f"{rng.choice(atoms)} {rng.choice(cmps)} {rng.choice(atoms)}"
+            w = cmp()
+            if rng.uniform() < 0.4:
+                w = f"{w} {rng.choice(['AND', 'OR'])} {cmp()}"
+            v = pw.analyze_condition(w, stats)
+            if v == "unknown":
+                continue
+            decided += 1
+            _, idx = ora.project_filter(t, "a", w)
+            assert len(idx) == (n if v == "always_true" else 0), (w, v, len(idx))
+    assert decided > 50
     import subprocess
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))

@@ -279,6 +279,66 @@ def test_group_sum_reference_golden():
     assert sums[:4].cpu().tolist() == [15.25, 10.5, 20.0, 30.0]
 
 
+def _nan_minus_zero(n, seed):
+    """float32 values with NaNs, -0.0 and ties (MIN / MAX edge cases)."""
+    u = synth.uniform_f32(n, seed + 100, 0.0, 1.0)
+    v = np.round(synth.uniform_f32(n, seed, -50.0, 50.0), 1).astype(np.float32)
+    v[u < 0.02] = np.nan
+    v[(u >= 0.02) & (u < 0.05)] = np.float32(-0.0)
+    return v
+
+
+@pytest.mark.parametrize("cond,ocond", [(None, None), ("(price[idx] > 20.0f)", "price > 20"),
+                                        ("(price[idx] > 1000.0f)", "price > 1000")])
+def test_reduce_stats_vs_oracle(cond, ocond):
+    # ungrouped SUM / COUNT / MIN / MAX (query_sql aggregates, optimizer stats)
+    n = 1_000_003
+    cols = {"price": synth.uniform_f32(n, 1, 0.0, 40.0), "v": _nan_minus_zero(n, 5)}
+    table, _ = dev_table(cols)
+    for expr, oexpr in (("(price[idx] * 0.9f)", "price * 0.9"), ("v[idx]", "v")):
+        s, c, mn, mx = wx.reduce_stats(table, expr, cond, launch())
+        rs, rc, rmn, rmx = ora.stats(ora.HostTable(cols), oexpr, ocond)
+        assert c == rc
+        assert (s == rs) or (np.isnan(s) and np.isnan(rs))
+        assert np.array_equal(bits(np.float32(mn)), bits(rmn)) or (np.isnan(mn) and np.isnan(rmn))
+        assert np.array_equal(bits(np.float32(mx)), bits(rmx)) or (np.isnan(mx) and np.isnan(rmx))
+    # the plain SUM entry point is unchanged by the MIN / MAX build
+    s2, c2 = wx.reduce_sum(table, "(price[idx] * 0.9f)", cond, launch())
+    assert (s2, c2) == ora.reduce_sum(ora.HostTable(cols), "price * 0.9", ocond)
+
+
+def test_group_agg_minmax_vs_oracle():
+    n = 600_001
+    rng = np.random.default_rng(3)
+    keys_pool = np.concatenate([np.arange(0, 1024, dtype=np.int32),
+                                np.array([-7, 2048, 99_999, -(1 << 31)], np.int32)])
+    cols = {"v": _nan_minus_zero(n, 7), "k": rng.choice(keys_pool, n).astype(np.int32),
+            "price": synth.uniform_f32(n, 1, 0.0, 40.0)}
+    table, _ = dev_table(cols)
+    cap = 2048
+    keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+    sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+    mins = torch.empty(cap, dtype=torch.float32, device="cuda")
+    maxs = torch.empty(cap, dtype=torch.float32, device="cuda")
+    for cond, ocond in ((None, None), ("(price[idx] < 10.0f)", "price < 10"), (None, None)):
+        g = wx.group_agg(table, "v[idx]", "k[idx]", cond, launch(), 0, cap, keys.data_ptr(), sums.data_ptr(),
+                         cnts.data_ptr(), mins.data_ptr(), maxs.data_ptr())
+        rk, rs, rc, rmn, rmx = ora.group_agg(ora.HostTable(cols), "v", "k", ocond)
+        assert g == len(rk)
+        assert np.array_equal(keys[:g].cpu().numpy(), rk)
+        assert np.array_equal(cnts[:g].cpu().numpy(), rc)
+        assert np.array_equal(sums[:g].cpu().numpy(), rs, equal_nan=True)
+        assert np.array_equal(mins[:g].cpu().numpy(), rmn, equal_nan=True)
+        assert np.array_equal(maxs[:g].cpu().numpy(), rmx, equal_nan=True)
+        assert not np.signbit(mins[:g].cpu().numpy()[mins[:g].cpu().numpy() == 0]).any()
+    # a plain GROUP BY SUM after MIN / MAX calls sees clean tables
+    g = wx.group_sum(table, "price[idx]", "k[idx]", None, launch(), 0, cap, keys.data_ptr(), sums.data_ptr(),
+                     cnts.data_ptr())
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "k")
+    assert g == len(rk) and np.array_equal(sums[:g].cpu().numpy(), rs)
+
+
 def test_group_capacity_error():
     cols = synth.c3_table(10_000)
     table, _ = dev_table(cols)

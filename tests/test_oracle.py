@@ -141,6 +141,29 @@ def test_group_sum_general_keys():
     assert c.sum() == 5000
 
 
+def test_stats_and_group_minmax_vs_numpy():
+    # AggData min / max (src/warpdb.cpp:375-385), stated NaN-skipping
+    rng = np.random.default_rng(8)
+    v = np.round(rng.uniform(-9, 9, 3000), 1).astype(np.float32)
+    v[rng.uniform(size=3000) < 0.05] = np.nan
+    k = rng.integers(0, 40, 3000).astype(np.int32)
+    t = ora.HostTable({"v": v, "k": k})
+    s, c, mn, mx = ora.stats(t, "v", "v > 2")
+    sel = v[v > 2]
+    assert c == len(sel) and mn == np.nanmin(sel) and mx == np.nanmax(sel)
+    keys, sums, cnts, mins, maxs = ora.group_agg(t, "v", "k")
+    for j, key in enumerate(keys):
+        g = v[k == key]
+        assert cnts[j] == len(g)
+        assert mins[j] == np.nanmin(g) and maxs[j] == np.nanmax(g)
+    # empty set -> NaN; -0.0 folds to +0.0
+    _, c0, mn0, mx0 = ora.stats(t, "v", "v > 100")
+    assert c0 == 0 and np.isnan(mn0) and np.isnan(mx0)
+    z = ora.HostTable({"z": np.array([-0.0, 0.0, -0.0], np.float32)})
+    _, _, zmn, zmx = ora.stats(z, "z")
+    assert not np.signbit(zmn) and not np.signbit(zmx)
+
+
 REF = ora.REF_HARNESS
 
 

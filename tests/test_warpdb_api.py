@@ -102,6 +102,51 @@ def test_query_sql_reference_expectations():
     assert db.query_sql("SELECT price * 2 FROM test WHERE quantity > 3") == [40.0, 60.0]
 
 
+def test_query_sql_min_max():
+    # AggData min / max (src/warpdb.cpp:375-385, 387-418) on data/test.csv:
+    # price [10.5, 20, 15.25, 30], quantity [3, 4, 2, 5]
+    db = pw().WarpDB(TEST_CSV)
+    assert db.query_sql("SELECT MIN(price) FROM test") == [10.5]
+    assert db.query_sql("SELECT MAX(price) FROM test WHERE quantity < 5") == [20.0]
+    assert db.query_sql("SELECT MAX(price) FROM test GROUP BY quantity ORDER BY quantity ASC") == \
+        [15.25, 10.5, 20.0, 30.0]
+    assert db.query_sql("SELECT SUM(price) FROM test GROUP BY quantity HAVING MIN(price) > 12 "
+                        "ORDER BY quantity ASC") == [15.25, 20.0, 30.0]
+    assert db.query_sql("SELECT MIN(price * quantity) FROM test GROUP BY quantity ORDER BY MIN(price * quantity) "
+                        "DESC LIMIT 2") == [150.0, 80.0]
+    r = db.query_sql("SELECT MIN(price) FROM test WHERE price > 100")
+    assert len(r) == 1 and r[0] != r[0]  # empty -> NaN (SQL NULL)
+
+
+def test_optimizer_stats_pushdown(tmp_path):
+    db = pw().WarpDB(TEST_CSV)
+    st = db.column_stats()
+    assert st["price"] == (10.5, 30.0, 0, False) and st["quantity"] == (2.0, 5.0, 0, False)
+    r, v = db.query_optimized("price * quantity WHERE price > 100")
+    assert v == "always_false" and r == [0.0, 0.0, 0.0, 0.0]
+    r, v = db.query_optimized("price * quantity WHERE price > 10")
+    assert v == "always_true" and r == [31.5, 80.0, 30.5, 150.0]
+    r, v = db.query_optimized("price * quantity WHERE price > 15")
+    assert v == "unknown" and r == db.query("price * quantity WHERE price > 15")
+    # statistics of a larger table (with NaN) against numpy
+    n = 100_003
+    cols = synth.c2_table(n)
+    cols["price"][::97] = np.nan
+    path = tmp_path / "s.csv"
+    with open(path, "w") as f:
+        f.write("price,quantity\n")
+        for p, q in zip(cols["price"], cols["quantity"]):
+            f.write(f"{float(p)!r},{int(q)}\n")
+    big = pw().WarpDB(str(path))
+    st = big.column_stats()
+    p = cols["price"]
+    assert st["price"] == (float(np.nanmin(p)), float(np.nanmax(p)), int(np.isnan(p).sum()), False)
+    r, v = big.query_optimized("price WHERE price >= 0", st)
+    assert v == "unknown"  # NaN rows fail the comparison
+    r, v = big.query_optimized("price WHERE quantity >= 1", st)
+    assert v == "always_true"
+
+
 def test_query_arrow_roundtrip():
     pa = pytest.importorskip("pyarrow")
     db = pw().WarpDB(TEST_CSV)

@@ -42,7 +42,9 @@ OP_DENSE, OP_COMPACT, OP_SUM, OP_GROUP, OP_TOPK, OP_UTIL = 0, 1, 2, 3, 4, 5
 EXPORTED_SYMBOLS = (
     "wx_project_filter",
     "wx_reduce_sum",
+    "wx_reduce_stats",
     "wx_group_sum",
+    "wx_group_agg",
     "wx_topk",
     "wx_sort_pairs",
     "wx_sort_float",
@@ -62,6 +64,11 @@ class WxCol(ctypes.Structure):
 
 class WxTable(ctypes.Structure):
     _fields_ = [("n_rows", ctypes.c_int64), ("n_cols", ctypes.c_int32), ("cols", ctypes.POINTER(WxCol))]
+
+
+class WxStats(ctypes.Structure):
+    _fields_ = [("sum", ctypes.c_double), ("count", ctypes.c_int64), ("min", ctypes.c_float),
+                ("max", ctypes.c_float)]
 
 
 class WxLaunch(ctypes.Structure):
@@ -103,7 +110,9 @@ def load() -> ctypes.CDLL:
     sig = {
         "wx_project_filter": [T, E, E, L, I32, P, P, I32, I64, P, pI64, E, S],
         "wx_reduce_sum": [T, E, E, L, P, pD, pI64, E, S],
+        "wx_reduce_stats": [T, E, E, L, P, ctypes.POINTER(WxStats), E, S],
         "wx_group_sum": [T, E, E, E, L, I32, I64, P, P, P, P, pI64, E, S],
+        "wx_group_agg": [T, E, E, E, L, I32, I64, P, P, P, P, P, P, pI64, E, S],
         "wx_topk": [T, E, E, E, I32, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_sort_pairs": [P, P, I64, I32, L, E, S],
         "wx_sort_float": [P, I64, I32, L, E, S],
@@ -218,6 +227,32 @@ def group_sum(table: Table, val_expr: str, key_expr: str, cond: Optional[str], l
                           ctypes.byref(launch), key_window_lo, capacity, d_keys or None, d_sums or None,
                           d_counts or None, d_n_groups or None, ctypes.byref(h) if want_count else None,
                           err, len(err))
+    _check(st, err)
+    return h.value if want_count else None
+
+
+def reduce_stats(table: Table, expr: str, cond: Optional[str], launch: WxLaunch, d_out: int = 0,
+                 want_host: bool = True):
+    """(sum, count, min, max) of (float)expr WHERE cond; MIN / MAX skip NaN, NaN when empty."""
+    lib = load()
+    err = _err()
+    h = WxStats()
+    st = lib.wx_reduce_stats(ctypes.byref(table.c), _enc(expr), _enc(cond), ctypes.byref(launch), d_out or None,
+                             ctypes.byref(h) if want_host else None, err, len(err))
+    _check(st, err)
+    return (h.sum, h.count, h.min, h.max) if want_host else None
+
+
+def group_agg(table: Table, val_expr: str, key_expr: str, cond: Optional[str], launch: WxLaunch,
+              key_window_lo: int, capacity: int, d_keys: int, d_sums: int, d_counts: int, d_mins: int = 0,
+              d_maxs: int = 0, d_n_groups: int = 0, want_count: bool = True) -> Optional[int]:
+    lib = load()
+    err = _err()
+    h = ctypes.c_int64(-1)
+    st = lib.wx_group_agg(ctypes.byref(table.c), _enc(val_expr), _enc(key_expr), _enc(cond),
+                          ctypes.byref(launch), key_window_lo, capacity, d_keys or None, d_sums or None,
+                          d_counts or None, d_mins or None, d_maxs or None, d_n_groups or None,
+                          ctypes.byref(h) if want_count else None, err, len(err))
     _check(st, err)
     return h.value if want_count else None
 

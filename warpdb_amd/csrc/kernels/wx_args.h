@@ -60,6 +60,8 @@ struct WxSumArgs {
   const void *col[WX_MAX_COLS];
   double *part_sum;  // [gridDim.x]
   wx_i64 *part_cnt;  // [gridDim.x]
+  wx_u32 *part_min;  // [gridDim.x] order-mapped (WX_MINMAX builds)
+  wx_u32 *part_max;  // [gridDim.x]
   wx_i64 n_rows;
 };
 
@@ -73,6 +75,10 @@ struct WxGroupArgs {
   wx_u64 *h_cnt;    // [hcap]
   wx_u32 *h_used;   // [hcap] slots taken, in insertion order
   wx_u64 *ctrs;     // [0] used slots, [1] error bits
+  wx_u32 *win_min;  // [WX_GROUP_WINDOW] order-mapped, ~0 = none (WX_MINMAX builds)
+  wx_u32 *win_max;  // [WX_GROUP_WINDOW] order-mapped, 0 = none
+  wx_u32 *h_min;    // [hcap]
+  wx_u32 *h_max;    // [hcap]
   wx_u32 hmask;     // hcap - 1 (hcap a power of two)
   int key_lo;
 };
@@ -85,9 +91,15 @@ struct WxGroupFinArgs {
   wx_u64 *h_cnt;
   wx_u32 *h_used;
   wx_u64 *ctrs;
+  wx_u32 *win_min;
+  wx_u32 *win_max;
+  wx_u32 *h_min;
+  wx_u32 *h_max;
   int *out_keys;
   double *out_sums;
   wx_i64 *out_counts;
+  float *out_mins;  // nullable
+  float *out_maxs;  // nullable
   wx_i64 *n_groups_out;
   wx_i64 capacity;
   int key_lo;
@@ -150,7 +162,9 @@ struct WxSortApplyArgs {
 struct WxSumFinArgs {
   const double *part_sum;
   const wx_i64 *part_cnt;
-  double *out;  // {sum, count bits}
+  const wx_u32 *part_min;
+  const wx_u32 *part_max;
+  double *out;  // wx_stats: {sum f64, count i64, min f32, max f32} (min/max in WX_MINMAX builds)
   int n_parts;
 };
 

@@ -595,47 +595,109 @@ extern "C" __global__ __launch_bounds__(WX_DTHREADS) void wx_project_compact_tic
 #ifndef WX_UNROLL
 #define WX_UNROLL 8  // tools/ablate_stream.py: 8 quads in flight, 8 workgroups per CU
 #endif
+#ifndef WX_MINMAX
+#define WX_MINMAX 0  // also MIN / MAX of the passing values (NaN skipped)
+#endif
+namespace wx {
+__device__ __forceinline__ wx_u32 wave_min_u32(wx_u32 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const wx_u32 x = __shfl_xor(v, o); v = x < v ? x : v; }
+  return v;
+}
+__device__ __forceinline__ wx_u32 wave_max_u32(wx_u32 v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) { const wx_u32 x = __shfl_xor(v, o); v = x > v ? x : v; }
+  return v;
+}
+// decoded MIN / MAX; an empty set (no non-NaN value) reads as NaN (SQL NULL)
+__device__ __forceinline__ float minmax_out(wx_u32 m, bool is_min) {
+  return (is_min ? m == 0xffffffffu : m == 0u) ? __uint_as_float(0x7fc00000u) : ord2f(m);
+}
+}  // namespace wx
+
 extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_reduce_sum(WxSumArgs wx_a) {
   __shared__ double s_sum[WX_WAVES];
   __shared__ wx_i64 s_cnt[WX_WAVES];
+  __shared__ wx_u32 s_min[WX_WAVES], s_max[WX_WAVES];
   double wx_acc = 0.0;
   wx_i64 wx_cnt = 0;
+  wx_u32 wx_mn = 0xffffffffu, wx_mx = 0u;
   WX_STRIDE_LOOP_BEGIN
   const bool wx_k = idx < wx_a.n_rows && WX_EVAL_COND();
   const float wx_val = static_cast<float>(WX_EXPR);
   wx_acc += wx_k ? (double)wx_val : 0.0;
   wx_cnt += wx_k ? 1 : 0;
+  if (WX_MINMAX) {
+    const wx_u32 o = wx::f2ord(wx_val);  // NaN -> 0
+    const bool in = wx_k && o != 0u;
+    wx_mn = (in && o < wx_mn) ? o : wx_mn;
+    wx_mx = (in && o > wx_mx) ? o : wx_mx;
+  }
   WX_STRIDE_LOOP_END
   double acc = wx::wave_sum_f64(wx_acc);
   wx_i64 cnt = (wx_i64)wx::wave_sum_u64((wx_u64)wx_cnt);
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) { s_sum[wave] = acc; s_cnt[wave] = cnt; }
+  if (WX_MINMAX) {
+    wx_mn = wx::wave_min_u32(wx_mn);
+    wx_mx = wx::wave_max_u32(wx_mx);
+  }
+  if (lane == 0) { s_sum[wave] = acc; s_cnt[wave] = cnt; s_min[wave] = wx_mn; s_max[wave] = wx_mx; }
   __syncthreads();
   if (threadIdx.x == 0) {
     double s = 0.0;
     wx_i64 c = 0;
-    for (int w = 0; w < WX_WAVES; ++w) { s += s_sum[w]; c += s_cnt[w]; }
+    wx_u32 mn = 0xffffffffu, mx = 0u;
+    for (int w = 0; w < WX_WAVES; ++w) {
+      s += s_sum[w];
+      c += s_cnt[w];
+      mn = s_min[w] < mn ? s_min[w] : mn;
+      mx = s_max[w] > mx ? s_max[w] : mx;
+    }
     wx_a.part_sum[blockIdx.x] = s;
     wx_a.part_cnt[blockIdx.x] = c;
+    if (WX_MINMAX) {
+      wx_a.part_min[blockIdx.x] = mn;
+      wx_a.part_max[blockIdx.x] = mx;
+    }
   }
 }
 
 extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sum_finalize(WxSumFinArgs a) {
   __shared__ double s_sum[WX_BLOCK];
   __shared__ wx_i64 s_cnt[WX_BLOCK];
+  __shared__ wx_u32 s_min[WX_BLOCK], s_max[WX_BLOCK];
   double s = 0.0;
   wx_i64 c = 0;
-  for (int i = threadIdx.x; i < a.n_parts; i += WX_BLOCK) { s += a.part_sum[i]; c += a.part_cnt[i]; }
+  wx_u32 mn = 0xffffffffu, mx = 0u;
+  for (int i = threadIdx.x; i < a.n_parts; i += WX_BLOCK) {
+    s += a.part_sum[i];
+    c += a.part_cnt[i];
+    if (WX_MINMAX) {
+      mn = a.part_min[i] < mn ? a.part_min[i] : mn;
+      mx = a.part_max[i] > mx ? a.part_max[i] : mx;
+    }
+  }
   s_sum[threadIdx.x] = s;
   s_cnt[threadIdx.x] = c;
+  s_min[threadIdx.x] = mn;
+  s_max[threadIdx.x] = mx;
   __syncthreads();
   for (int w = WX_BLOCK / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) { s_sum[threadIdx.x] += s_sum[threadIdx.x + w]; s_cnt[threadIdx.x] += s_cnt[threadIdx.x + w]; }
+    if ((int)threadIdx.x < w) {
+      s_sum[threadIdx.x] += s_sum[threadIdx.x + w];
+      s_cnt[threadIdx.x] += s_cnt[threadIdx.x + w];
+      s_min[threadIdx.x] = s_min[threadIdx.x + w] < s_min[threadIdx.x] ? s_min[threadIdx.x + w] : s_min[threadIdx.x];
+      s_max[threadIdx.x] = s_max[threadIdx.x + w] > s_max[threadIdx.x] ? s_max[threadIdx.x + w] : s_max[threadIdx.x];
+    }
     __syncthreads();
   }
   if (threadIdx.x == 0) {
     a.out[0] = s_sum[0];
     reinterpret_cast<wx_i64 *>(a.out)[1] = s_cnt[0];
+    if (WX_MINMAX) {
+      reinterpret_cast<float *>(a.out)[4] = wx::minmax_out(s_min[0], true);
+      reinterpret_cast<float *>(a.out)[5] = wx::minmax_out(s_max[0], false);
+    }
   }
 }
 #endif
@@ -656,7 +718,14 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sum_finalize(WxSumFinA
 #endif
 #define WX_HSORT_MAX WX_GROUP_HSORT_MAX
 
-__device__ __forceinline__ void wx_hash_add(const WxGroupArgs &a, int key, double v) {
+#ifndef WX_MINMAX
+#define WX_MINMAX 0  // also per-group MIN / MAX (NaN skipped)
+#endif
+__device__ __forceinline__ float wx_mm_out(wx_u32 m, bool is_min) {
+  return (is_min ? m == 0xffffffffu : m == 0u) ? __uint_as_float(0x7fc00000u) : wx::ord2f(m);
+}
+
+__device__ __forceinline__ void wx_hash_add(const WxGroupArgs &a, int key, double v, wx_u32 o) {
   const wx_u64 tag = (wx_u64)(wx_u32)key | (1ull << 32);
   wx_u32 h = ((wx_u32)key * 2654435761u) & a.hmask;
   for (wx_u32 probe = 0; probe <= a.hmask; ++probe) {
@@ -674,6 +743,10 @@ __device__ __forceinline__ void wx_hash_add(const WxGroupArgs &a, int key, doubl
     if (cur == tag) {
       atomicAdd(&a.h_sum[h], v);
       atomicAdd(&a.h_cnt[h], 1ull);
+      if (WX_MINMAX && o != 0u) {
+        atomicMin(&a.h_min[h], o);
+        atomicMax(&a.h_max[h], o);
+      }
       return;
     }
     h = (h + 1) & a.hmask;
@@ -684,18 +757,35 @@ __device__ __forceinline__ void wx_hash_add(const WxGroupArgs &a, int key, doubl
 extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs wx_a) {
   __shared__ double wx_s_sum[WX_GWIN];
   __shared__ wx_u32 wx_s_cnt[WX_GWIN];
-  for (int i = threadIdx.x; i < WX_GWIN; i += WX_BLOCK) { wx_s_sum[i] = 0.0; wx_s_cnt[i] = 0u; }
+#if WX_MINMAX
+  __shared__ wx_u32 wx_s_min[WX_GWIN], wx_s_max[WX_GWIN];
+#endif
+  for (int i = threadIdx.x; i < WX_GWIN; i += WX_BLOCK) {
+    wx_s_sum[i] = 0.0;
+    wx_s_cnt[i] = 0u;
+#if WX_MINMAX
+    wx_s_min[i] = 0xffffffffu;
+    wx_s_max[i] = 0u;
+#endif
+  }
   __syncthreads();
   WX_STRIDE_LOOP_BEGIN
   if (idx < wx_a.n_rows && WX_EVAL_COND()) {
     const int wx_key = static_cast<int>(WX_KEY);
     const float wx_val = static_cast<float>(WX_EXPR);
     const wx_u32 wx_bin = (wx_u32)(wx_key - wx_a.key_lo);
+    const wx_u32 wx_o = WX_MINMAX ? wx::f2ord(wx_val) : 0u;  // NaN -> 0: skipped
     if (wx_bin < (wx_u32)WX_GWIN) {
       atomicAdd(&wx_s_sum[wx_bin], (double)wx_val);
       atomicAdd(&wx_s_cnt[wx_bin], 1u);
+#if WX_MINMAX
+      if (wx_o != 0u) {
+        atomicMin(&wx_s_min[wx_bin], wx_o);
+        atomicMax(&wx_s_max[wx_bin], wx_o);
+      }
+#endif
     } else {
-      wx_hash_add(wx_a, wx_key, (double)wx_val);
+      wx_hash_add(wx_a, wx_key, (double)wx_val, wx_o);
     }
   }
   WX_STRIDE_LOOP_END
@@ -705,6 +795,12 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs 
     if (c) {
       atomicAdd(&wx_a.win_sum[i], wx_s_sum[i]);
       atomicAdd(&wx_a.win_cnt[i], (wx_u64)c);
+#if WX_MINMAX
+      if (wx_s_max[i] != 0u) {
+        atomicMin(&wx_a.win_min[i], wx_s_min[i]);
+        atomicMax(&wx_a.win_max[i], wx_s_max[i]);
+      }
+#endif
     }
   }
 }
@@ -773,8 +869,19 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroup
       a.out_keys[pos] = a.key_lo + b;
       a.out_sums[pos] = a.win_sum[b];
       a.out_counts[pos] = (wx_i64)c;
+#if WX_MINMAX
+      if (a.out_mins) a.out_mins[pos] = wx_mm_out(a.win_min[b], true);
+      if (a.out_maxs) a.out_maxs[pos] = wx_mm_out(a.win_max[b], false);
+#endif
     }
-    if (b < WX_GWIN && c) { a.win_sum[b] = 0.0; a.win_cnt[b] = 0ull; }
+    if (b < WX_GWIN && c) {
+      a.win_sum[b] = 0.0;
+      a.win_cnt[b] = 0ull;
+#if WX_MINMAX
+      a.win_min[b] = 0xffffffffu;
+      a.win_max[b] = 0u;
+#endif
+    }
     out_pos += s_scan[WX_BLOCK - 1];
     __syncthreads();
   }
@@ -787,6 +894,10 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroup
       a.out_keys[pos] = (int)((wx_u32)(e >> 32) ^ 0x80000000u);
       a.out_sums[pos] = a.h_sum[slot];
       a.out_counts[pos] = (wx_i64)a.h_cnt[slot];
+#if WX_MINMAX
+      if (a.out_mins) a.out_mins[pos] = wx_mm_out(a.h_min[slot], true);
+      if (a.out_maxs) a.out_maxs[pos] = wx_mm_out(a.h_max[slot], false);
+#endif
     }
   }
   __syncthreads();
@@ -797,6 +908,10 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroup
     a.h_tag[slot] = 0ull;
     a.h_sum[slot] = 0.0;
     a.h_cnt[slot] = 0ull;
+#if WX_MINMAX
+    a.h_min[slot] = 0xffffffffu;
+    a.h_max[slot] = 0u;
+#endif
   }
   if (tid == 0) {
     a.ctrs[0] = 0ull;

@@ -6,11 +6,39 @@
 #include <pybind11/stl.h>
 
 #include "warpdb/multi_gpu_utils.hpp"
+#include "warpdb/optimizer.hpp"
 #include "warpdb/warpdb.hpp"
 
 namespace py = pybind11;
 
 namespace {
+py::dict stats_to_dict(const warpdb::StatsMap &m) {
+  py::dict d;
+  for (const auto &kv : m) {
+    const auto &r = kv.second;
+    d[py::str(kv.first)] = py::make_tuple(r.known ? py::cast(r.min) : py::none(),
+                                          r.known ? py::cast(r.max) : py::none(), r.null_count, r.is_int);
+  }
+  return d;
+}
+
+// {name: (min, max, null_count, is_int)}; min/max None = unbounded
+warpdb::StatsMap stats_from_dict(const py::dict &d) {
+  warpdb::StatsMap m;
+  for (auto item : d) {
+    auto t = item.second.cast<py::tuple>();
+    warpdb::ColumnRange r;
+    r.known = !t[0].is_none() && !t[1].is_none();
+    if (r.known) {
+      r.min = t[0].cast<double>();
+      r.max = t[1].cast<double>();
+    }
+    r.null_count = t.size() > 2 ? t[2].cast<int64_t>() : 0;
+    r.is_int = t.size() > 3 ? t[3].cast<bool>() : false;
+    m[item.first.cast<std::string>()] = r;
+  }
+  return m;
+}
 py::tuple arrow_capsules(ArrowArray *arr, ArrowSchema *schema) {
   py::capsule a(arr, [](void *p) {
     auto *x = static_cast<ArrowArray *>(p);
@@ -65,12 +93,50 @@ PYBIND11_MODULE(pywarpdb, m) {
       .def("query_compact", &WarpDB::query_compact, py::call_guard<py::gil_scoped_release>())
       .def("query_sum", &WarpDB::query_sum, py::call_guard<py::gil_scoped_release>())
       .def("query_multi_gpu_sum", &WarpDB::query_multi_gpu_sum, py::call_guard<py::gil_scoped_release>())
+      .def(
+          "column_stats",
+          [](const WarpDB &db) {
+            warpdb::StatsMap m;
+            {
+              py::gil_scoped_release nogil;
+              m = warpdb::compute_column_stats(db.table());
+            }
+            return stats_to_dict(m);
+          },
+          "Per-column (min, max, null_count, is_int) as the kernels see the values (optimizer statistics).")
+      .def(
+          "query_optimized",
+          [](const WarpDB &db, const std::string &q, py::object stats) {
+            std::string e, c;
+            warpdb::split_where(q, e, c);
+            warpdb::StatsMap m;
+            const bool have = !stats.is_none();
+            if (have) m = stats_from_dict(stats.cast<py::dict>());
+            warpdb::Verdict v;
+            std::vector<float> r;
+            {
+              py::gil_scoped_release nogil;
+              r = warpdb::query_optimized(e, c, db.table(), have ? &m : nullptr, &v);
+            }
+            return py::make_tuple(r, warpdb::verdict_name(v));
+          },
+          py::arg("query"), py::arg("stats") = py::none(),
+          "Dense projection with statistics pushdown -> (values, verdict).")
       .def_property_readonly("num_rows", [](const WarpDB &db) { return db.table().num_rows; })
       .def_property_readonly("column_names", [](const WarpDB &db) {
         std::vector<std::string> n;
         for (const auto &c : db.table().columns) n.push_back(c.name);
         return n;
       });
+
+  m.def(
+      "analyze_condition",
+      [](const std::string &where, const py::dict &stats) {
+        auto ast = parse_expression(tokenize(where));
+        return std::string(warpdb::verdict_name(warpdb::analyze_condition(ast.get(), stats_from_dict(stats))));
+      },
+      py::arg("where"), py::arg("stats"),
+      "Interval analysis of a WHERE clause over {column: (min, max, null_count, is_int)}.");
 
   // front end, for tests and tools
   m.def("lower_expression", [](const std::string &e) { return parse_expression(tokenize(e))->to_cuda_expr(); });

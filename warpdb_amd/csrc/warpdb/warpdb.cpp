@@ -237,6 +237,16 @@ std::vector<float> WarpDB::query_multi_gpu_csv(const std::string &csv_path, cons
 }
 
 // ------------------------------------------------------------------ SQL
+namespace {
+bool uses_minmax(const ASTNode *n) {
+  if (!n) return false;
+  if (auto a = dynamic_cast<const AggregationNode *>(n))
+    return a->agg == AggregationType::Min || a->agg == AggregationType::Max;
+  if (auto b = dynamic_cast<const BinaryOpNode *>(n)) return uses_minmax(b->left.get()) || uses_minmax(b->right.get());
+  return false;
+}
+}  // namespace
+
 std::vector<float> WarpDB::query_sql(const std::string &sql) {
   QueryAST ast;
   try {
@@ -281,31 +291,43 @@ std::vector<float> WarpDB::query_sql(const std::string &sql) {
     if (ast.group_by->keys.size() != 1) throw std::runtime_error("GROUP BY supports one key expression");
     const ASTNode *key = ast.group_by->keys[0].get();
     const int64_t cap = std::max<int64_t>(1, std::min<int64_t>(table_.num_rows, 1 << 22));
+    // MIN / MAX anywhere (SELECT, HAVING, ORDER BY) selects the MIN / MAX build
+    const bool mm = uses_minmax(agg) || (ast.having && uses_minmax(ast.having->get())) ||
+                    (ast.order_by && uses_minmax(ast.order_by->expr.get()));
     DeviceBuffer dk(table_.device, cap * 4), ds(table_.device, cap * 8), dc(table_.device, cap * 8);
+    DeviceBuffer dmn(table_.device, mm ? cap * 4 : 4), dmx(table_.device, mm ? cap * 4 : 4);
     int64_t g = 0;
-    throw_on(wx_group_sum(&v.table, agg->expr->to_cuda_expr().c_str(), key->to_cuda_expr().c_str(), cond.c_str(), &L,
+    throw_on(wx_group_agg(&v.table, agg->expr->to_cuda_expr().c_str(), key->to_cuda_expr().c_str(), cond.c_str(), &L,
                           0, cap, static_cast<int32_t *>(dk.ptr), static_cast<double *>(ds.ptr),
-                          static_cast<int64_t *>(dc.ptr), nullptr, &g, err, sizeof(err)),
+                          static_cast<int64_t *>(dc.ptr), mm ? static_cast<float *>(dmn.ptr) : nullptr,
+                          mm ? static_cast<float *>(dmx.ptr) : nullptr, nullptr, &g, err, sizeof(err)),
              err);
     std::vector<int32_t> keys(g);
     std::vector<double> sums(g);
     std::vector<int64_t> cnts(g);
+    std::vector<float> mins(mm ? g : 0), maxs(mm ? g : 0);
     {
       DevGuard dg(table_.device);
       if (g) {
         hip_ok(hipMemcpy(keys.data(), dk.ptr, g * 4, hipMemcpyDeviceToHost), "hipMemcpy");
         hip_ok(hipMemcpy(sums.data(), ds.ptr, g * 8, hipMemcpyDeviceToHost), "hipMemcpy");
         hip_ok(hipMemcpy(cnts.data(), dc.ptr, g * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+        if (mm) {
+          hip_ok(hipMemcpy(mins.data(), dmn.ptr, g * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+          hip_ok(hipMemcpy(maxs.data(), dmx.ptr, g * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+        }
       }
     }
-    // per-group aggregate value; MIN / MAX need reducers the engine lacks
+    // per-group aggregate value (AggData, src/warpdb.cpp:375-385)
     auto value_of = [&](AggregationType t, size_t i) -> double {
       switch (t) {
         case AggregationType::Sum: return sums[i];
         case AggregationType::Avg: return sums[i] / static_cast<double>(cnts[i]);
         case AggregationType::Count: return static_cast<double>(cnts[i]);
-        default: throw std::runtime_error("MIN/MAX aggregation is not supported by the execution engine");
+        case AggregationType::Min: return mins[i];
+        case AggregationType::Max: return maxs[i];
       }
+      return NAN;
     };
     // HAVING over the (few) aggregated groups, with the reference's
     // comparison semantics (src/warpdb.cpp:387-423)
@@ -361,17 +383,23 @@ std::vector<float> WarpDB::query_sql(const std::string &sql) {
   }
 
   if (agg) {  // ungrouped aggregate over the WHERE rows
-    double s = 0;
-    int64_t n = 0;
-    throw_on(wx_reduce_sum(&v.table, agg->expr->to_cuda_expr().c_str(), cond.c_str(), &L, nullptr, &s, &n, err,
-                           sizeof(err)),
-             err);
-    double val;
+    wx_stats st{};
+    if (uses_minmax(agg)) {
+      throw_on(wx_reduce_stats(&v.table, agg->expr->to_cuda_expr().c_str(), cond.c_str(), &L, nullptr, &st, err,
+                               sizeof(err)),
+               err);
+    } else {
+      throw_on(wx_reduce_sum(&v.table, agg->expr->to_cuda_expr().c_str(), cond.c_str(), &L, nullptr, &st.sum,
+                             &st.count, err, sizeof(err)),
+               err);
+    }
+    double val = NAN;
     switch (agg->agg) {
-      case AggregationType::Sum: val = s; break;
-      case AggregationType::Avg: val = n ? s / n : NAN; break;
-      case AggregationType::Count: val = static_cast<double>(n); break;
-      default: throw std::runtime_error("MIN/MAX aggregation is not supported by the execution engine");
+      case AggregationType::Sum: val = st.sum; break;
+      case AggregationType::Avg: val = st.count ? st.sum / static_cast<double>(st.count) : NAN; break;
+      case AggregationType::Count: val = static_cast<double>(st.count); break;
+      case AggregationType::Min: val = st.min; break;
+      case AggregationType::Max: val = st.max; break;
     }
     return slice({static_cast<float>(val)});
   }
