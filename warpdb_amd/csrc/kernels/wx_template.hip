@@ -662,41 +662,67 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_reduce_sum(WxSumArgs w
   }
 }
 
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sum_finalize(WxSumFinArgs a) {
-  __shared__ double s_sum[WX_BLOCK];
-  __shared__ wx_i64 s_cnt[WX_BLOCK];
-  __shared__ wx_u32 s_min[WX_BLOCK], s_max[WX_BLOCK];
+// One 1024-thread block combines the per-workgroup partials in a fixed order
+// (bitwise reproducible): loads batched four per thread, wave reductions,
+// then the sixteen wave results in order.
+#define WX_SFIN_BLOCK 1024
+extern "C" __global__ __launch_bounds__(WX_SFIN_BLOCK) void wx_sum_finalize(WxSumFinArgs a) {
+  __shared__ double s_sum[WX_SFIN_BLOCK / 64];
+  __shared__ wx_i64 s_cnt[WX_SFIN_BLOCK / 64];
+  __shared__ wx_u32 s_min[WX_SFIN_BLOCK / 64], s_max[WX_SFIN_BLOCK / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   double s = 0.0;
   wx_i64 c = 0;
   wx_u32 mn = 0xffffffffu, mx = 0u;
-  for (int i = threadIdx.x; i < a.n_parts; i += WX_BLOCK) {
-    s += a.part_sum[i];
-    c += a.part_cnt[i];
-    if (WX_MINMAX) {
-      mn = a.part_min[i] < mn ? a.part_min[i] : mn;
-      mx = a.part_max[i] > mx ? a.part_max[i] : mx;
+  for (int i0 = tid; i0 < a.n_parts; i0 += WX_SFIN_BLOCK * 4) {
+    double ps[4];
+    wx_i64 pc[4];
+    wx_u32 pmn[4], pmx[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = i0 + j * WX_SFIN_BLOCK;
+      const bool ok = i < a.n_parts;
+      ps[j] = ok ? a.part_sum[i] : 0.0;
+      pc[j] = ok ? a.part_cnt[i] : 0;
+      pmn[j] = (WX_MINMAX && ok) ? a.part_min[i] : 0xffffffffu;
+      pmx[j] = (WX_MINMAX && ok) ? a.part_max[i] : 0u;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      s += ps[j];
+      c += pc[j];
+      mn = pmn[j] < mn ? pmn[j] : mn;
+      mx = pmx[j] > mx ? pmx[j] : mx;
     }
   }
-  s_sum[threadIdx.x] = s;
-  s_cnt[threadIdx.x] = c;
-  s_min[threadIdx.x] = mn;
-  s_max[threadIdx.x] = mx;
+  s = wx::wave_sum_f64(s);
+  c = (wx_i64)wx::wave_sum_u64((wx_u64)c);
+  if (WX_MINMAX) {
+    mn = wx::wave_min_u32(mn);
+    mx = wx::wave_max_u32(mx);
+  }
+  if (lane == 0) {
+    s_sum[wave] = s;
+    s_cnt[wave] = c;
+    s_min[wave] = mn;
+    s_max[wave] = mx;
+  }
   __syncthreads();
-  for (int w = WX_BLOCK / 2; w > 0; w >>= 1) {
-    if ((int)threadIdx.x < w) {
-      s_sum[threadIdx.x] += s_sum[threadIdx.x + w];
-      s_cnt[threadIdx.x] += s_cnt[threadIdx.x + w];
-      s_min[threadIdx.x] = s_min[threadIdx.x + w] < s_min[threadIdx.x] ? s_min[threadIdx.x + w] : s_min[threadIdx.x];
-      s_max[threadIdx.x] = s_max[threadIdx.x + w] > s_max[threadIdx.x] ? s_max[threadIdx.x + w] : s_max[threadIdx.x];
+  if (tid == 0) {
+    double ts = 0.0;
+    wx_i64 tc = 0;
+    wx_u32 tmn = 0xffffffffu, tmx = 0u;
+    for (int w = 0; w < WX_SFIN_BLOCK / 64; ++w) {
+      ts += s_sum[w];
+      tc += s_cnt[w];
+      tmn = s_min[w] < tmn ? s_min[w] : tmn;
+      tmx = s_max[w] > tmx ? s_max[w] : tmx;
     }
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) {
-    a.out[0] = s_sum[0];
-    reinterpret_cast<wx_i64 *>(a.out)[1] = s_cnt[0];
+    a.out[0] = ts;
+    reinterpret_cast<wx_i64 *>(a.out)[1] = tc;
     if (WX_MINMAX) {
-      reinterpret_cast<float *>(a.out)[4] = wx::minmax_out(s_min[0], true);
-      reinterpret_cast<float *>(a.out)[5] = wx::minmax_out(s_max[0], false);
+      reinterpret_cast<float *>(a.out)[4] = wx::minmax_out(tmn, true);
+      reinterpret_cast<float *>(a.out)[5] = wx::minmax_out(tmx, false);
     }
   }
 }
@@ -805,11 +831,15 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs 
   }
 }
 
-// One block: sort the general-key entries, merge with the dense window in
-// ascending key order, write the outputs, zero what was used.
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroupFinArgs a) {
+// One 1024-thread block: sort the general-key entries, merge with the dense
+// window in ascending key order, write the outputs, zero what was used.  The
+// window is two adjacent bins per thread, all loaded up front (one round trip
+// to the accumulators the atomics left beyond L2), ranked by one block scan.
+#define WX_GFIN_BLOCK 1024
+static_assert(WX_GWIN == 2 * WX_GFIN_BLOCK, "two window bins per finalize thread");
+extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(WxGroupFinArgs a) {
   __shared__ wx_u64 s_ent[WX_HSORT_MAX];  // (key ^ sign) << 32 | used-list position
-  __shared__ wx_u32 s_scan[WX_BLOCK];
+  __shared__ wx_u32 s_wtot[WX_GFIN_BLOCK / 64];
   __shared__ wx_i64 s_nlo;
   const int tid = threadIdx.x;
   const wx_i64 n_hash = (wx_i64)a.ctrs[0];
@@ -820,7 +850,10 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroup
   const int nh = too_many ? 0 : (int)n_hash;
   int npad = 1;
   while (npad < nh) npad <<= 1;
-  for (int i = tid; i < npad; i += WX_BLOCK) {
+  // window bins of this thread, loaded before the (rare) hash-key sort
+  const int b0 = tid * 2;
+  const wx_u64 wc0 = a.win_cnt[b0], wc1 = a.win_cnt[b0 + 1];
+  for (int i = tid; i < npad; i += WX_GFIN_BLOCK) {
     wx_u64 e = ~0ull;
     if (i < nh) {
       const wx_u32 slot = a.h_used[i];
@@ -832,7 +865,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroup
   __syncthreads();
   for (int k = 2; k <= npad; k <<= 1)
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < npad; i += WX_BLOCK) {
+      for (int i = tid; i < npad; i += WX_GFIN_BLOCK) {
         const int p = i ^ j;
         if (p > i) {
           const wx_u64 x = s_ent[i], y = s_ent[p];
@@ -850,43 +883,52 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroup
   }
   __syncthreads();
   const wx_i64 nlo = s_nlo;
-  // dense window compaction (ascending bins), block-wide scan in chunks
-  wx_i64 out_pos = nlo;
-  for (int base = 0; base < WX_GWIN; base += WX_BLOCK) {
-    const int b = base + tid;
-    const wx_u64 c = (b < WX_GWIN) ? a.win_cnt[b] : 0ull;
-    const wx_u32 f = c ? 1u : 0u;
-    s_scan[tid] = f;
-    __syncthreads();
-    for (int o = 1; o < WX_BLOCK; o <<= 1) {
-      const wx_u32 t = (tid >= o) ? s_scan[tid - o] : 0u;
-      __syncthreads();
-      s_scan[tid] += t;
-      __syncthreads();
-    }
-    const wx_i64 pos = out_pos + s_scan[tid] - f;
-    if (f && pos < a.capacity) {
-      a.out_keys[pos] = a.key_lo + b;
-      a.out_sums[pos] = a.win_sum[b];
-      a.out_counts[pos] = (wx_i64)c;
+  // dense window compaction (ascending bins): wave scan + wave totals
+  const int lane = tid & 63, wave = tid >> 6;
+  const wx_u32 f = (wc0 ? 1u : 0u) + (wc1 ? 1u : 0u);
+  wx_u32 incl = f;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const wx_u32 t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_wtot[wave] = incl;
+  __syncthreads();
+  wx_u32 wbase = 0, wsum = 0;
+#pragma unroll
+  for (int w = 0; w < WX_GFIN_BLOCK / 64; ++w) {
+    const wx_u32 v = s_wtot[w];
+    wbase += (w < wave) ? v : 0u;
+    wsum += v;
+  }
+  {
+    wx_i64 pos = nlo + wbase + incl - f;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int b = b0 + h;
+      const wx_u64 c = h ? wc1 : wc0;
+      if (!c) continue;
+      if (pos < a.capacity) {
+        a.out_keys[pos] = a.key_lo + b;
+        a.out_sums[pos] = a.win_sum[b];
+        a.out_counts[pos] = (wx_i64)c;
 #if WX_MINMAX
-      if (a.out_mins) a.out_mins[pos] = wx_mm_out(a.win_min[b], true);
-      if (a.out_maxs) a.out_maxs[pos] = wx_mm_out(a.win_max[b], false);
+        if (a.out_mins) a.out_mins[pos] = wx_mm_out(a.win_min[b], true);
+        if (a.out_maxs) a.out_maxs[pos] = wx_mm_out(a.win_max[b], false);
 #endif
-    }
-    if (b < WX_GWIN && c) {
+      }
       a.win_sum[b] = 0.0;
       a.win_cnt[b] = 0ull;
 #if WX_MINMAX
       a.win_min[b] = 0xffffffffu;
       a.win_max[b] = 0u;
 #endif
+      ++pos;
     }
-    out_pos += s_scan[WX_BLOCK - 1];
-    __syncthreads();
   }
+  const wx_i64 out_pos = nlo + wsum;
   // hash entries: below-window ones first, the rest after the window
-  for (int i = tid; i < nh; i += WX_BLOCK) {
+  for (int i = tid; i < nh; i += WX_GFIN_BLOCK) {
     const wx_u64 e = s_ent[i];
     const wx_u32 slot = a.h_used[(wx_u32)e];
     const wx_i64 pos = (i < nlo) ? (wx_i64)i : out_pos + (i - nlo);
@@ -903,7 +945,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_finalize(WxGroup
   __syncthreads();
   const wx_i64 total = out_pos + (nh - nlo);
   // return the general-key table to its clean state
-  for (wx_i64 i = tid; i < n_hash; i += WX_BLOCK) {
+  for (wx_i64 i = tid; i < n_hash; i += WX_GFIN_BLOCK) {
     const wx_u32 slot = a.h_used[i];
     a.h_tag[slot] = 0ull;
     a.h_sum[slot] = 0.0;
@@ -1031,19 +1073,15 @@ __device__ __forceinline__ void block_merge(TopList &L, wx_u32 (*s_k)[WX_TOPK_K]
     for (int j = 0; j < WX_TOPK_K; ++j) { s_k[wave][j] = wk[j]; s_i[wave][j] = wi[j]; }
   }
   __syncthreads();
-  if (wave == 0) {
-    int head[NW];
+  if (wave == 0) {  // lane w holds wave w's sorted list: one more wave merge
+    static_assert(NW <= 64, "one lane per wave");
+    TopList M;
+    M.init();
+    if (lane < NW) {
 #pragma unroll
-    for (int w = 0; w < NW; ++w) head[w] = 0;
-    for (int r = 0; r < WX_TOPK_K; ++r) {
-      int best = 0;
-      for (int w = 1; w < NW; ++w)
-        if (better(s_k[w][head[w]], s_i[w][head[w]], s_k[best][head[best]], s_i[best][head[best]])) best = w;
-      bk[r] = s_k[best][head[best]];
-      bi[r] = s_i[best][head[best]];
-      if (head[best] < WX_TOPK_K - 1) ++head[best];
-      else { s_k[best][head[best]] = 0u; s_i[best][head[best]] = WX_IDX_NONE; }
+      for (int j = 0; j < WX_TOPK_K; ++j) { M.k[j] = s_k[lane][j]; M.i[j] = s_i[lane][j]; }
     }
+    wave_merge(M, bk, bi);
   }
 }
 }  // namespace wx
