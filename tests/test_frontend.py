@@ -142,6 +142,9 @@ def test_optimizer_is_sound_against_oracle():
             _, idx = ora.project_filter(t, "a", w)
             assert len(idx) == (n if v == "always_true" else 0), (w, v, len(idx))
     assert decided > 50
+
+
+def test_cpp_frontend_binary():
     import subprocess
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -152,3 +155,63 @@ def test_optimizer_is_sound_against_oracle():
                        text=True, cwd=root)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "frontend_test: all passed" in r.stdout
+
+
+def _libc():
+    import ctypes
+
+    c = ctypes.CDLL(None)
+    c.strtof.restype = ctypes.c_float
+    c.strtof.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p)]
+    c.strtoll.restype = ctypes.c_longlong
+    c.strtoll.argtypes = [ctypes.c_char_p, ctypes.POINTER(ctypes.c_char_p), ctypes.c_int]
+    return c
+
+
+def test_parallel_csv_parser_matches_strtof(tmp_path):
+    # the loader keeps the sequential std::strto* meaning of every cell
+    # (src/csv_loader.cpp:49-124) while parsing line ranges in parallel
+    import numpy as np
+
+    rng = np.random.default_rng(5)
+    odd = ["+1.5", " 2", "0x10", "1e3", "inf", "-inf", "-0", ".5", "7.", "3.4028236e38", "1e-46", "12abc",
+           "  -4.25", "1E+2"]
+    n = 60_000
+    vals = []
+    for i in range(n):
+        if i % 97 == 0:
+            vals.append(odd[(i // 97) % len(odd)])
+        else:
+            vals.append(repr(float(np.float32(rng.uniform(-1e4, 1e4)))))
+    ints = rng.integers(-(1 << 40), 1 << 40, n)
+    path = tmp_path / "p.csv"
+    with open(path, "w", newline="") as f:
+        f.write("a,b,s\r\n")
+        for i in range(n):
+            if i % 1000 == 0:
+                f.write("\r\n")  # blank lines are skipped
+            f.write(f"{vals[i]},{ints[i]},w{i}\r\n" if i % 3 else f"{vals[i]},{ints[i]},w{i}\n")
+    schema = [pw.DataType.Float32, pw.DataType.Int64, pw.DataType.String]
+    c = _libc()
+    want_a = np.array([c.strtof(v.encode(), None) for v in vals], np.float32)
+    for threads in (1, 3, 16):
+        d = pw.load_csv_columns(str(path), schema, threads)
+        assert np.array_equal(d["a"].view(np.uint32), want_a.view(np.uint32)), threads
+        assert np.array_equal(d["b"], ints)
+        assert d["s"][:3] == ["w0", "w1", "w2"] and len(d["s"]) == n
+
+
+def test_csv_parser_errors(tmp_path):
+    p = tmp_path / "bad.csv"
+    p.write_text("a,b\n1,2\n3,abc\n")
+    with pytest.raises(RuntimeError, match="Invalid numeric value in CSV: 'abc'"):
+        pw.load_csv_columns(str(p))
+    p.write_text("a,b\n1,2\n3\n")  # a missing cell is an empty cell
+    with pytest.raises(RuntimeError, match="Invalid numeric value in CSV: ''"):
+        pw.load_csv_columns(str(p))
+    p.write_text("a,b\n1,2,9\n")  # extra cells are ignored
+    d = pw.load_csv_columns(str(p))
+    assert d["a"].tolist() == [1.0] and d["b"].tolist() == [2.0]
+    # golden data files load as the reference does (default schema: all Float32)
+    d = pw.load_csv_columns(os.path.join(GOLDEN, "test.csv"))
+    assert d["price"].tolist() == [10.5, 20.0, 15.25, 30.0] and d["quantity"].tolist() == [3, 4, 2, 5]

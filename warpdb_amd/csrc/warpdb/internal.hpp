@@ -68,6 +68,20 @@ struct WxTableView {
   wx_table table{};
 };
 
+// Host <-> HBM copies (transfer.cpp).  copy_h2d may return before the DMA
+// finishes (the source is already staged); copy_d2h returns with `dst` filled.
+enum class TransferMode { Pageable, Staged, Register };
+TransferMode transfer_mode();  // $WARPDB_H2D: pageable | staged (default) | register
+void copy_h2d(int device, hipStream_t s, void *dst, const void *src, size_t bytes);
+void copy_d2h(int device, hipStream_t s, void *dst, const void *src, size_t bytes);
+// A zero-filled host result of n floats (huge-page backed when large).
+std::vector<float> host_result(size_t n);
+
+// CSV data rows in [b, e) appended to `out` (typed columns already set up),
+// parsed on up to `threads` threads (csv_parse.cpp).
+int parse_threads();  // $WARPDB_PARSE_THREADS, default hardware threads, at most 16
+void parse_csv_rows(const char *b, const char *e, HostTable &out, int threads);
+
 wx_launch sync_launch(int device, void *stream = nullptr);
 void throw_on(wx_status st, const char *err);
 

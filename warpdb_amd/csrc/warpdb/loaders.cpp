@@ -2,9 +2,12 @@
 // Semantics follow the reference loaders (src/csv_loader.cpp:49-223,
 // src/json_loader.cpp:16-53): header row of names, default schema all
 // Float32, one value per comma-separated cell.
+#include <fcntl.h>
 #include <hip/hip_runtime_api.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
 
-#include <cerrno>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
@@ -12,6 +15,7 @@
 #include <stdexcept>
 
 #include "warpdb/csv_loader.hpp"
+#include "internal.hpp"
 #include "warpdb/json_loader.hpp"
 
 namespace {
@@ -43,43 +47,6 @@ ColumnData empty_column(DataType t) {
   return std::vector<float>();
 }
 
-// std::sto* semantics: leading blanks skipped, trailing text ignored, an
-// empty or non-numeric cell is an error.
-[[noreturn]] void bad_cell(const std::string &v) { throw std::runtime_error("Invalid numeric value in CSV: '" + v + "'"); }
-
-void append_cell(HostColumn &col, const std::string &v) {
-  const char *s = v.c_str();
-  char *end = nullptr;
-  errno = 0;
-  switch (col.type) {
-    case DataType::Int32: {
-      long x = std::strtol(s, &end, 10);
-      if (end == s || errno == ERANGE || x < INT32_MIN || x > INT32_MAX) bad_cell(v);
-      std::get<std::vector<int32_t>>(col.data).push_back(static_cast<int32_t>(x));
-      break;
-    }
-    case DataType::Int64: {
-      long long x = std::strtoll(s, &end, 10);
-      if (end == s || errno == ERANGE) bad_cell(v);
-      std::get<std::vector<int64_t>>(col.data).push_back(x);
-      break;
-    }
-    case DataType::Float32: {
-      float x = std::strtof(s, &end);
-      if (end == s) bad_cell(v);
-      std::get<std::vector<float>>(col.data).push_back(x);
-      break;
-    }
-    case DataType::Float64: {
-      double x = std::strtod(s, &end);
-      if (end == s) bad_cell(v);
-      std::get<std::vector<double>>(col.data).push_back(x);
-      break;
-    }
-    case DataType::String: std::get<std::vector<std::string>>(col.data).push_back(v); break;
-  }
-}
-
 HostTable make_table(const std::vector<std::string> &names, const std::vector<DataType> &schema) {
   if (!schema.empty() && schema.size() != names.size())
     throw std::runtime_error("Schema size does not match column count");
@@ -89,15 +56,6 @@ HostTable make_table(const std::vector<std::string> &names, const std::vector<Da
     h.columns.push_back({names[i], t, empty_column(t)});
   }
   return h;
-}
-
-void append_row(HostTable &h, const std::string &line) {
-  std::stringstream ss(line);
-  std::string cell;
-  for (auto &col : h.columns) {
-    if (!std::getline(ss, cell, ',')) cell.clear();
-    append_cell(col, cell);
-  }
 }
 
 size_t width(DataType t) {
@@ -117,18 +75,33 @@ const void *host_data(const HostColumn &c) {
 }  // namespace
 
 HostTable load_csv_to_host(const std::string &filepath, const std::vector<DataType> &schema) {
-  std::ifstream file(filepath);
-  if (!file.is_open()) throw std::runtime_error("Unable to open file: " + filepath);
-  std::string header;
-  if (!std::getline(file, header)) throw std::runtime_error("Empty CSV file");
+  // the whole file is mapped and its rows parsed in parallel
+  const int fd = ::open(filepath.c_str(), O_RDONLY);
+  if (fd < 0) throw std::runtime_error("Unable to open file: " + filepath);
+  struct stat st;
+  if (::fstat(fd, &st) != 0) {
+    ::close(fd);
+    throw std::runtime_error("Unable to open file: " + filepath);
+  }
+  const size_t size = static_cast<size_t>(st.st_size);
+  if (size == 0) {
+    ::close(fd);
+    throw std::runtime_error("Empty CSV file");
+  }
+  void *map = ::mmap(nullptr, size, PROT_READ, MAP_PRIVATE, fd, 0);
+  ::close(fd);
+  if (map == MAP_FAILED) throw std::runtime_error("Unable to map file: " + filepath);
+  struct Unmap {
+    void *p;
+    size_t n;
+    ~Unmap() { ::munmap(p, n); }
+  } unmap{map, size};
+  const char *b = static_cast<const char *>(map), *e = b + size;
+  const char *nl = static_cast<const char *>(std::memchr(b, '\n', size));
+  std::string header(b, nl ? nl : e);
   strip_cr(header);
   HostTable h = make_table(split_commas(header), schema);
-  std::string line;
-  while (std::getline(file, line)) {
-    strip_cr(line);
-    if (line.empty()) continue;
-    append_row(h, line);
-  }
+  if (nl) warpdb::parse_csv_rows(nl + 1, e, h, warpdb::parse_threads());
   return h;
 }
 
@@ -146,12 +119,12 @@ Table upload_to_gpu(const HostTable &host, int device) {
       if (w && t.num_rows > 0) {
         hip_check(hipMalloc(&p, w * static_cast<size_t>(t.num_rows)), "hipMalloc");
         t.columns.push_back({c.name, c.type, p, t.num_rows});
-        hip_check(hipMemcpy(p, host_data(c), w * static_cast<size_t>(t.num_rows), hipMemcpyHostToDevice),
-                  "hipMemcpy");
+        warpdb::copy_h2d(device, nullptr, p, host_data(c), w * static_cast<size_t>(t.num_rows));
       } else {
         t.columns.push_back({c.name, c.type, nullptr, t.num_rows});  // strings stay on the host
       }
     }
+    hip_check(hipStreamSynchronize(nullptr), "hipStreamSynchronize");
   } catch (...) {
     free_table(t);
     (void)hipSetDevice(prev);
@@ -179,15 +152,17 @@ void free_table(Table &t) {
 HostTable load_csv_chunk(std::istream &stream, int64_t max_rows, bool &finished, const std::vector<std::string> &names,
                          const std::vector<DataType> &schema) {
   HostTable h = make_table(names, schema);
-  std::string line;
+  // gather up to max_rows non-empty lines, then parse them in parallel
+  std::string text, line;
   int64_t n = 0;
   while (n < max_rows && std::getline(stream, line)) {
     strip_cr(line);
     if (line.empty()) continue;
-    append_row(h, line);
+    text.append(line).push_back('\n');
     ++n;
   }
   finished = !stream.good();
+  warpdb::parse_csv_rows(text.data(), text.data() + text.size(), h, warpdb::parse_threads());
   return h;
 }
 

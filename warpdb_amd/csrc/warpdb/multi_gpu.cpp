@@ -12,6 +12,7 @@
 #include <algorithm>
 #include <cstring>
 #include <exception>
+#include <future>
 #include <mutex>
 #include <stdexcept>
 #include <thread>
@@ -63,8 +64,7 @@ Shard upload_shard(const HostTable &h, int device, int64_t b, int64_t e, hipStre
     const size_t w = width(c.type);
     sh.bufs.emplace_back(device, w * static_cast<size_t>(e - b));
     const char *src = static_cast<const char *>(std::visit([](auto &&v) -> const void * { return v.data(); }, c.data));
-    hip_ok(hipMemcpyAsync(sh.bufs.back().ptr, src + w * b, w * static_cast<size_t>(e - b), hipMemcpyHostToDevice, s),
-           "hipMemcpyAsync");
+    copy_h2d(device, s, sh.bufs.back().ptr, src + w * b, w * static_cast<size_t>(e - b));
     sh.table.columns.push_back({c.name, c.type, sh.bufs.back().ptr, e - b});
   }
   return sh;
@@ -182,8 +182,24 @@ std::vector<float> run_multi_gpu_jit_host(const HostTable &host, const std::stri
                                           const std::string &cond_cuda) {
   using namespace warpdb;
   const int64_t n = host.num_rows();
-  std::vector<float> result(static_cast<size_t>(n), 0.0f);
   auto shards = plan_shards(n, device_count());
+  // The host result (4 B/row, first-touch bound) is allocated on its own
+  // thread while the devices upload and compute; D2H waits for it.
+  std::vector<float> result;
+  std::promise<void> ready;
+  std::shared_future<void> result_ready = ready.get_future().share();
+  std::thread alloc([&] {
+    try {
+      result = host_result(static_cast<size_t>(n));
+      ready.set_value();
+    } catch (...) {
+      ready.set_exception(std::current_exception());
+    }
+  });
+  struct Join {
+    std::thread &t;
+    ~Join() { t.join(); }
+  } join{alloc};
   run_per_device(shards, [&](size_t, const ShardRange &r) {
     hipStream_t s = device_stream(r.device);
     Shard sh = upload_shard(host, r.device, r.begin, r.end, s);
@@ -195,11 +211,10 @@ std::vector<float> run_multi_gpu_jit_host(const HostTable &host, const std::stri
     throw_on(wx_project_filter(&v.table, expr_cuda.c_str(), cond_cuda.c_str(), &L, WX_MODE_DENSE_FILL,
                                static_cast<float *>(out.ptr), nullptr, 0, 0, nullptr, nullptr, err, sizeof(err)),
              err);
-    hip_ok(hipMemcpyAsync(result.data() + r.begin, out.ptr, sizeof(float) * static_cast<size_t>(r.end - r.begin),
-                          hipMemcpyDeviceToHost, s),
-           "hipMemcpyAsync");
-    hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize");
+    result_ready.get();
+    copy_d2h(r.device, s, result.data() + r.begin, out.ptr, sizeof(float) * static_cast<size_t>(r.end - r.begin));
     throw_on(wx_check(&L, err, sizeof(err)), err);
   });
+  result_ready.get();  // n == 0: no device ran
   return result;
 }

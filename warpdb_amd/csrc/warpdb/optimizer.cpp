@@ -302,10 +302,10 @@ std::vector<float> query_optimized(const std::string &expr_part, const std::stri
   throw_on(wx_project_filter(&v.table, expr.c_str(), cond.c_str(), &L, WX_MODE_DENSE_FILL,
                              static_cast<float *>(out.ptr), nullptr, 0, 0, nullptr, nullptr, err, sizeof(err)),
            err);
-  std::vector<float> h(static_cast<size_t>(n));
+  std::vector<float> h = host_result(static_cast<size_t>(n));
   if (n) {
     DevGuard g(table.device);
-    hip_ok(hipMemcpy(h.data(), out.ptr, sizeof(float) * static_cast<size_t>(n), hipMemcpyDeviceToHost), "hipMemcpy");
+    copy_d2h(table.device, nullptr, h.data(), out.ptr, sizeof(float) * static_cast<size_t>(n));
   }
   return h;
 }

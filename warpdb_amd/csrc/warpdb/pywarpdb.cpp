@@ -2,6 +2,7 @@
 // (bindings/python/pywarpdb.cpp:7-38): WarpDB(path), query, query_multi_gpu,
 // query_multi_gpu_csv (static), query_arrow -> (array capsule, schema
 // capsule); plus query_sql / query_compact / query_sum and the front end.
+#include <pybind11/numpy.h>
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 
@@ -137,6 +138,33 @@ PYBIND11_MODULE(pywarpdb, m) {
       },
       py::arg("where"), py::arg("stats"),
       "Interval analysis of a WHERE clause over {column: (min, max, null_count, is_int)}.");
+
+  m.def(
+      "load_csv_columns",
+      [](const std::string &path, const std::vector<DataType> &schema, int threads) {
+        HostTable h;
+        {
+          py::gil_scoped_release nogil;
+          if (threads > 0) setenv("WARPDB_PARSE_THREADS", std::to_string(threads).c_str(), 1);
+          h = load_csv_to_host(path, schema);
+        }
+        py::dict d;
+        for (const auto &c : h.columns) {
+          std::visit(
+              [&](const auto &v) {
+                using T = typename std::decay_t<decltype(v)>::value_type;
+                if constexpr (std::is_same_v<T, std::string>) {
+                  d[py::str(c.name)] = py::cast(v);
+                } else {
+                  d[py::str(c.name)] = py::array_t<T>(static_cast<py::ssize_t>(v.size()), v.data());
+                }
+              },
+              c.data);
+        }
+        return d;
+      },
+      py::arg("path"), py::arg("schema") = std::vector<DataType>{}, py::arg("threads") = 0,
+      "Host-side CSV load (load_csv_to_host) as {column: numpy array | list}; no GPU needed.");
 
   // front end, for tests and tools
   m.def("lower_expression", [](const std::string &e) { return parse_expression(tokenize(e))->to_cuda_expr(); });

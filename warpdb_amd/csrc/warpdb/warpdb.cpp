@@ -9,11 +9,16 @@
 #include <algorithm>
 #include <cctype>
 #include <cmath>
+#include <condition_variable>
+#include <deque>
+#include <exception>
 #include <fstream>
 #include <functional>
 #include <map>
+#include <mutex>
 #include <sstream>
 #include <stdexcept>
+#include <thread>
 #include <unordered_set>
 
 #include "warpdb/internal.hpp"
@@ -97,9 +102,9 @@ std::string lower_ext(const std::string &path) {
 }
 
 std::vector<float> download(const void *d, int64_t n, int device) {
-  std::vector<float> h(static_cast<size_t>(n));
+  std::vector<float> h = warpdb::host_result(static_cast<size_t>(n));
   DevGuard g(device);
-  if (n) hip_ok(hipMemcpy(h.data(), d, sizeof(float) * static_cast<size_t>(n), hipMemcpyDeviceToHost), "hipMemcpy");
+  if (n) warpdb::copy_d2h(device, nullptr, h.data(), d, sizeof(float) * static_cast<size_t>(n));
   return h;
 }
 
@@ -225,14 +230,60 @@ std::vector<float> WarpDB::query_multi_gpu_csv(const std::string &csv_path, cons
   std::unordered_set<std::string> cols(names.begin(), names.end());
   std::string e, c;
   lower_query(expr, cols, e, c);
+  // Two-stage pipeline: a parser thread reads chunk i+1 while the GPUs run
+  // chunk i (the reference parses, uploads and runs each chunk in turn,
+  // src/warpdb.cpp:544-590).  At most two parsed chunks wait in the queue.
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<HostTable> ready;
+  bool done = false;
+  std::exception_ptr parse_err;
+  std::thread parser([&] {
+    try {
+      bool finished = false;
+      while (!finished) {
+        HostTable chunk = load_csv_chunk(file, static_cast<int64_t>(rows_per_chunk), finished, names);
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return ready.size() < 2 || done; });
+        if (done) break;  // consumer gave up
+        if (chunk.num_rows() == 0) break;
+        ready.push_back(std::move(chunk));
+        cv.notify_all();
+      }
+    } catch (...) {
+      std::lock_guard<std::mutex> lk(mu);
+      parse_err = std::current_exception();
+    }
+    std::lock_guard<std::mutex> lk(mu);
+    done = true;
+    cv.notify_all();
+  });
   std::vector<float> all;
-  bool finished = false;
-  while (!finished) {
-    HostTable chunk = load_csv_chunk(file, static_cast<int64_t>(rows_per_chunk), finished, names);
-    if (chunk.num_rows() == 0) break;
-    auto part = run_multi_gpu_jit_host(chunk, e, c);
-    all.insert(all.end(), part.begin(), part.end());
+  try {
+    while (true) {
+      HostTable chunk;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [&] { return !ready.empty() || done; });
+        if (ready.empty()) break;
+        chunk = std::move(ready.front());
+        ready.pop_front();
+        cv.notify_all();
+      }
+      auto part = run_multi_gpu_jit_host(chunk, e, c);
+      all.insert(all.end(), part.begin(), part.end());
+    }
+  } catch (...) {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      done = true;
+      cv.notify_all();
+    }
+    parser.join();
+    throw;
   }
+  parser.join();
+  if (parse_err) std::rethrow_exception(parse_err);
   return all;
 }
 
