@@ -41,6 +41,48 @@ __global__ __launch_bounds__(256) void read2(const v4f *__restrict__ a, const v4
 }
 
 template <int U, bool NT>
+__global__ __launch_bounds__(256) void read1(const v4f *__restrict__ a, size_t nq, float *out) {
+  float acc = 0.f;
+  size_t stride = (size_t)gridDim.x * 256;
+  size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  for (; i + (U - 1) * stride < nq; i += U * stride) {
+    v4f va[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) va[u] = NT ? __builtin_nontemporal_load(a + i + u * stride) : a[i + u * stride];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += va[u].x + va[u].y + va[u].z + va[u].w;
+  }
+  for (; i < nq; i += stride) acc += a[i].x;
+  if (acc == 1234.5f) out[0] = acc;
+}
+
+// block-contiguous: per iteration a workgroup reads U * 4 KiB in one span
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void read1c(const v4f *__restrict__ a, size_t nq, float *out) {
+  float acc = 0.f;
+  const size_t span = (size_t)256 * U;
+  for (size_t base = (size_t)blockIdx.x * span; base < nq; base += (size_t)gridDim.x * span) {
+    v4f va[U];
+    if (base + span <= nq) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t i = base + u * 256 + threadIdx.x;
+        va[u] = NT ? __builtin_nontemporal_load(a + i) : a[i];
+      }
+    } else {
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t i = base + u * 256 + threadIdx.x;
+        va[u] = i < nq ? a[i] : v4f{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += va[u].x + va[u].y + va[u].z + va[u].w;
+  }
+  if (acc == 1234.5f) out[0] = acc;
+}
+
+template <int U, bool NT>
 __global__ __launch_bounds__(256) void copy1(const v4f *__restrict__ a, v4f *__restrict__ o, size_t nq) {
   size_t stride = (size_t)gridDim.x * 256;
   size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -130,7 +172,7 @@ int main(int argc, char **argv) {
   CK(hipGetDeviceProperties(&pr, 0));
   cus = pr.multiProcessorCount;
   const int reps = 15;
-  int wpcs[] = {2, 4, 8, 16};
+  int wpcs[] = {1, 2, 3, 4, 8, 16};
 #define RUN(name, KER, bytes, ...)                                                                            \
   for (int w : wpcs) {                                                                                        \
     int g = cus * w;                                                                                          \
@@ -141,6 +183,14 @@ int main(int argc, char **argv) {
   RUN("read2 u8", (read2<8, false>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
   RUN("read2 u4 nt", (read2<4, true>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
   RUN("read2 u8 nt", (read2<8, true>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
+  RUN("read1 u4 nt", (read1<4, true>), n * 4, (const v4f *)a, nq, out);
+  RUN("read1 u8 nt", (read1<8, true>), n * 4, (const v4f *)a, nq, out);
+  RUN("read1 u16 nt", (read1<16, true>), n * 4, (const v4f *)a, nq, out);
+  RUN("read1 u8", (read1<8, false>), n * 4, (const v4f *)a, nq, out);
+  RUN("read1c u4 nt", (read1c<4, true>), n * 4, (const v4f *)a, nq, out);
+  RUN("read1c u8 nt", (read1c<8, true>), n * 4, (const v4f *)a, nq, out);
+  RUN("read1c u16 nt", (read1c<16, true>), n * 4, (const v4f *)a, nq, out);
+  RUN("read1 u4 nt again", (read1<4, true>), n * 4, (const v4f *)a, nq, out);
   RUN("copy u4", (copy1<4, false>), n * 8, (const v4f *)a, (v4f *)ov, nq);
   RUN("copy u4 nt", (copy1<4, true>), n * 8, (const v4f *)a, (v4f *)ov, nq);
   RUN("r2w u4", (r2w<4, false>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);

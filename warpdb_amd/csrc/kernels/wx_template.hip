@@ -167,9 +167,13 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 // one row's values (gathered at `idx`), bound like the streamed registers
 #define WX_BIND_ROW(name, T, slot) const ::wx::reg<T> name{static_cast<const T *>(wx_a.col[slot])[idx]};
 
-// Grid-stride kernels: WX_UNROLL row quads per thread per iteration, all
-// loads issued before any evaluation (a data-dependent branch in the
-// evaluation would otherwise stop the compiler from batching them).
+// Grid-stride kernels: per iteration a workgroup owns one contiguous span of
+// WX_BLOCK * WX_UNROLL row quads (thread t takes quads t, t + WX_BLOCK, ...
+// of the span) and issues all their loads before evaluating any row (a
+// data-dependent branch in the evaluation would otherwise stop the compiler
+// from batching them).  Contiguous spans keep the chip's loads in flight
+// within few DRAM pages: 6.7-6.85 TB/s at any grid size, against 5.6-6.9 for
+// quads a whole grid stride apart (tools/bw_probe.hip, read1c vs read1).
 #ifndef WX_STRIDE_SIMPLE
 #define WX_STRIDE_SIMPLE 0  // diagnostic: guarded loads only
 #endif
@@ -177,31 +181,31 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 #define WX_LOAD_U_FAST(name, T, slot) ::wx::load4_full<T>(wx_a.col[slot], wx_r0u, wx_u##slot[wx_u]);
 #define WX_LOAD_U(name, T, slot) ::wx::load4_tail<T>(wx_a.col[slot], wx_r0u, wx_a.n_rows, wx_u##slot[wx_u]);
 #define WX_BIND_U(name, T, slot) const ::wx::reg<T> name{wx_u##slot[wx_u][wx_e]};
-// When every quad of the workgroup's batch is complete (a workgroup-uniform
-// test) the loads are unconditional 16-byte loads; only the tail batch takes
-// the guarded path.
+#define WX_SPAN ((wx_i64)WX_BLOCK * WX_UNROLL)
+#define WX_QUAD(u) (wx_base + (wx_i64)(u) * WX_BLOCK + threadIdx.x)
+// When the whole span lies inside the table (a workgroup-uniform test) the
+// loads are unconditional 16-byte loads; only the last span takes the
+// guarded path.
 #define WX_STRIDE_LOOP_BEGIN                                                                             \
   const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;                                                           \
   const wx_i64 wx_nfull = wx_a.n_rows >> 2;                                                              \
-  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;                                                 \
-  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq;                        \
-       wx_q0 += wx_stride * WX_UNROLL) {                                                                 \
+  for (wx_i64 wx_base = (wx_i64)blockIdx.x * WX_SPAN; wx_base < wx_nq;                                   \
+       wx_base += (wx_i64)gridDim.x * WX_SPAN) {                                                         \
     WX_COLS(WX_DECL_U)                                                                                   \
-    const wx_i64 wx_qlast = wx_q0 - threadIdx.x + (WX_BLOCK - 1) + (WX_UNROLL - 1) * wx_stride;         \
-    if (WX_ALIGNED16 && !WX_STRIDE_SIMPLE && wx_qlast < wx_nfull) {                                      \
+    if (WX_ALIGNED16 && !WX_STRIDE_SIMPLE && wx_base + WX_SPAN <= wx_nfull) {                            \
       _Pragma("unroll") for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {                                  \
-        const wx_i64 wx_r0u = (wx_q0 + wx_u * wx_stride) << 2;                                           \
+        const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;                                                        \
         WX_COLS(WX_LOAD_U_FAST)                                                                          \
       }                                                                                                  \
     } else {                                                                                             \
       _Pragma("unroll") for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {                                  \
-        const wx_i64 wx_r0u = (wx_q0 + wx_u * wx_stride) << 2;                                           \
+        const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;                                                        \
         WX_COLS(WX_LOAD_U)                                                                               \
       }                                                                                                  \
     }                                                                                                    \
     _Pragma("unroll") for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {                                    \
-      const wx_i64 wx_r0 = (wx_q0 + wx_u * wx_stride) << 2;                                              \
-      if (wx_q0 + wx_u * wx_stride < wx_nq) {                                                            \
+      const wx_i64 wx_r0 = WX_QUAD(wx_u) << 2;                                                           \
+      if (WX_QUAD(wx_u) < wx_nq) {                                                                       \
         _Pragma("unroll") for (int wx_e = 0; wx_e < 4; ++wx_e) {                                        \
           WX_COLS(WX_BIND_U)                                                                             \
           const wx_i64 idx = wx_r0 + wx_e;
@@ -211,7 +215,7 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
   }                        \
   }
 // Closes the per-row loops but leaves the batch loop open: code after it
-// sees the whole batch (wx_q0, wx_stride); the caller closes the batch loop.
+// sees the whole span (wx_base, WX_QUAD); the caller closes the span loop.
 #define WX_STRIDE_BATCH_END \
   }                         \
   }                         \
@@ -1100,21 +1104,19 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
   float wx_T = wx_none;  // wave threshold: best worst-key over the wave's full lanes
   const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
   const wx_i64 wx_nfull = wx_a.n_rows >> 2;
-  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
-  for (wx_i64 wx_q0 = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q0 < wx_nq; wx_q0 += wx_stride * WX_UNROLL) {
+  for (wx_i64 wx_base = (wx_i64)blockIdx.x * WX_SPAN; wx_base < wx_nq; wx_base += (wx_i64)gridDim.x * WX_SPAN) {
     WX_COLS(WX_DECL_U)
-    const wx_i64 wx_qlast = wx_q0 - threadIdx.x + (WX_BLOCK - 1) + (WX_UNROLL - 1) * wx_stride;
-    const bool wx_whole = WX_ALIGNED16 && wx_qlast < wx_nfull;  // workgroup-uniform
+    const bool wx_whole = WX_ALIGNED16 && wx_base + WX_SPAN <= wx_nfull;  // workgroup-uniform
     if (wx_whole) {
 #pragma unroll
       for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
-        const wx_i64 wx_r0u = (wx_q0 + wx_u * wx_stride) << 2;
+        const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;
         WX_COLS(WX_LOAD_U_FAST)
       }
     } else {
 #pragma unroll
       for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
-        const wx_i64 wx_r0u = (wx_q0 + wx_u * wx_stride) << 2;
+        const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;
         WX_COLS(WX_LOAD_U)
       }
     }
@@ -1129,7 +1131,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
 #pragma unroll
         for (int wx_e = 0; wx_e < 4; ++wx_e) {
           WX_COLS(WX_BIND_U)
-          const wx_i64 idx = ((wx_q0 + wx_u * wx_stride) << 2) + wx_e;
+          const wx_i64 idx = (WX_QUAD(wx_u) << 2) + wx_e;
           (void)idx;
           const float wx_v = WX_EVAL_COND() ? static_cast<float>(WX_EXPR) : wx_none;
           wx_m = WX_TOPK_DESC ? fmaxf(wx_m, wx_v) : fminf(wx_m, wx_v);
@@ -1142,11 +1144,11 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
     if (wx_slow) {
 #pragma unroll
       for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
-        if (wx_q0 + wx_u * wx_stride < wx_nq) {
+        if (WX_QUAD(wx_u) < wx_nq) {
 #pragma unroll
           for (int wx_e = 0; wx_e < 4; ++wx_e) {
             WX_COLS(WX_BIND_U)
-            const wx_i64 idx = ((wx_q0 + wx_u * wx_stride) << 2) + wx_e;
+            const wx_i64 idx = (WX_QUAD(wx_u) << 2) + wx_e;
             if (idx < wx_a.n_rows && WX_EVAL_COND()) {
               const float wx_f = static_cast<float>(WX_EXPR);
               if (!(WX_TOPK_DESC ? wx_f < wx_T : wx_f > wx_T)) wx_L.offer(wx_f, idx);
