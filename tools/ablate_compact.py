@@ -43,6 +43,11 @@ VARIANTS = {
     "dw15_ntst": {"WARPDB_EXTRA_DEFINES": "WX_NT_STORE=1"},
     "dw15_plainld_ntst": {"WARPDB_EXTRA_DEFINES": "WX_NT_LOAD=0,WX_NT_STORE=1"},
     "dw12_ntst": {"WARPDB_COMPACT_DWAVES": "12", "WARPDB_EXTRA_DEFINES": "WX_NT_STORE=1"},
+    "v0_w0": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=0,WX_COMPACT_WHOLE_LOADS=0"},
+    "v1_w0": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=0"},
+    "v0_w1": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=0,WX_COMPACT_WHOLE_LOADS=1"},
+    "v1_w1": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=1"},
+    "v1_w0_dw12": {"WARPDB_COMPACT_DWAVES": "12", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=0"},
 }
 if len(sys.argv) > 3:
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in sys.argv[3].split(",")}

@@ -134,6 +134,85 @@ __global__ __launch_bounds__(256) void r2w(const v4f *__restrict__ a, const v4f 
   }
 }
 
+// block-contiguous read 8 B + write 5 B per row (compaction mix)
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void r2wc(const v4f *__restrict__ a, const v4f *__restrict__ b,
+                                            v4f *__restrict__ ov, v4u *__restrict__ oi, size_t nq) {
+  const size_t span = (size_t)256 * U;
+  for (size_t base = (size_t)blockIdx.x * span; base + span <= nq; base += (size_t)gridDim.x * span) {
+    v4f va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * 256 + threadIdx.x;
+      va[u] = NT ? __builtin_nontemporal_load(a + i) : a[i];
+      vb[u] = NT ? __builtin_nontemporal_load(b + i) : b[i];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t j = base + u * 256 + threadIdx.x;
+      if ((j & 7) < 5) {
+        const size_t p = (j >> 3) * 5 + (j & 7);
+        ov[p] = va[u] * vb[u];
+        oi[p] = (v4u){(unsigned)j * 4, (unsigned)j * 4 + 1, (unsigned)j * 4 + 2, (unsigned)j * 4 + 3};
+      }
+    }
+  }
+}
+
+// block-contiguous, output written as one dense run per span (like a
+// compacted tile): lanes store consecutive 16-B words of the span's output
+template <int U>
+__global__ __launch_bounds__(256) void r2wd(const v4f *__restrict__ a, const v4f *__restrict__ b,
+                                            v4f *__restrict__ ov, v4u *__restrict__ oi, size_t nq) {
+  const size_t span = (size_t)256 * U;
+  const size_t ospan = span * 5 / 8;
+  for (size_t base = (size_t)blockIdx.x * span, ob = (size_t)blockIdx.x * ospan; base + span <= nq;
+       base += (size_t)gridDim.x * span, ob += (size_t)gridDim.x * ospan) {
+    v4f va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * 256 + threadIdx.x;
+      va[u] = __builtin_nontemporal_load(a + i);
+      vb[u] = __builtin_nontemporal_load(b + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t k = u * 256 + threadIdx.x;
+      if (k < ospan) {
+        ov[ob + k] = va[u] * vb[u];
+        oi[ob + k] = (v4u){(unsigned)k, (unsigned)k + 1, (unsigned)k + 2, (unsigned)k + 3};
+      }
+    }
+  }
+}
+
+// as r2wd, but the output run is written with 4-byte stores (one value per
+// lane, like the compaction's LDS drain), starting `shift` floats past a
+// 16-byte boundary
+template <int U>
+__global__ __launch_bounds__(256) void r2wd4(const v4f *__restrict__ a, const v4f *__restrict__ b,
+                                             float *__restrict__ ov, unsigned *__restrict__ oi, size_t nq, int shift) {
+  const size_t span = (size_t)256 * U;
+  const size_t orows = span * 4 * 5 / 8;  // output values per span
+  for (size_t base = (size_t)blockIdx.x * span, ob = (size_t)blockIdx.x * orows + shift; base + span <= nq;
+       base += (size_t)gridDim.x * span, ob += (size_t)gridDim.x * orows) {
+    v4f va[U], vb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const size_t i = base + u * 256 + threadIdx.x;
+      va[u] = __builtin_nontemporal_load(a + i);
+      vb[u] = __builtin_nontemporal_load(b + i);
+    }
+    float acc = 0.f;
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc += va[u].x * vb[u].y + va[u].z * vb[u].w;
+    for (size_t k = threadIdx.x; k < orows; k += 256) {
+      ov[ob + k] = acc + (float)k;
+      oi[ob + k] = (unsigned)(base * 4 + k);
+    }
+  }
+}
+
 template <typename F>
 float time_it(F f, int reps) {
   hipEvent_t e0, e1;
@@ -172,7 +251,7 @@ int main(int argc, char **argv) {
   CK(hipGetDeviceProperties(&pr, 0));
   cus = pr.multiProcessorCount;
   const int reps = 15;
-  int wpcs[] = {1, 2, 3, 4, 8, 16};
+  int wpcs[] = {1, 2, 4, 8};
 #define RUN(name, KER, bytes, ...)                                                                            \
   for (int w : wpcs) {                                                                                        \
     int g = cus * w;                                                                                          \
@@ -180,21 +259,14 @@ int main(int argc, char **argv) {
     printf("%-28s wg/CU %2d  %7.3f ms  %7.1f GB/s\n", name, w, ms, (double)(bytes) / ms / 1e6);               \
   }
   RUN("read2 u4", (read2<4, false>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
-  RUN("read2 u8", (read2<8, false>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
-  RUN("read2 u4 nt", (read2<4, true>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
-  RUN("read2 u8 nt", (read2<8, true>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
-  RUN("read1 u4 nt", (read1<4, true>), n * 4, (const v4f *)a, nq, out);
-  RUN("read1 u8 nt", (read1<8, true>), n * 4, (const v4f *)a, nq, out);
-  RUN("read1 u16 nt", (read1<16, true>), n * 4, (const v4f *)a, nq, out);
-  RUN("read1 u8", (read1<8, false>), n * 4, (const v4f *)a, nq, out);
-  RUN("read1c u4 nt", (read1c<4, true>), n * 4, (const v4f *)a, nq, out);
   RUN("read1c u8 nt", (read1c<8, true>), n * 4, (const v4f *)a, nq, out);
-  RUN("read1c u16 nt", (read1c<16, true>), n * 4, (const v4f *)a, nq, out);
-  RUN("read1 u4 nt again", (read1<4, true>), n * 4, (const v4f *)a, nq, out);
-  RUN("copy u4", (copy1<4, false>), n * 8, (const v4f *)a, (v4f *)ov, nq);
   RUN("copy u4 nt", (copy1<4, true>), n * 8, (const v4f *)a, (v4f *)ov, nq);
-  RUN("r2w u4", (r2w<4, false>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
   RUN("r2w u4 nt", (r2w<4, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
-  RUN("r2w u8 nt", (r2w<8, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+  RUN("r2wc u8 nt", (r2wc<8, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+  RUN("r2wd u8", (r2wd<8>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+  RUN("r2wd4 u8 aligned", (r2wd4<8>), n * 13, (const v4f *)a, (const v4f *)b, ov, oi, nq, 0);
+  RUN("r2wd4 u8 shift3", (r2wd4<8>), n * 13, (const v4f *)a, (const v4f *)b, ov, oi, nq, 3);
+  RUN("r2wd4 u16 shift3", (r2wd4<16>), n * 13, (const v4f *)a, (const v4f *)b, ov, oi, nq, 3);
+  RUN("r2wd u16", (r2wd<16>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
   return 0;
 }

@@ -296,6 +296,14 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 #define WX_FLAG_A (1ull << 62)
 #define WX_FLAG_P (2ull << 62)
 #define WX_VAL_MASK ((1ull << 62) - 1ull)
+#ifndef WX_COMPACT_VSTORE
+#define WX_COMPACT_VSTORE 1  // 16-byte aligned stores for the output runs (2.65 -> 2.47 ms)
+#endif
+#ifndef WX_COMPACT_WHOLE_LOADS
+// unguarded loads when the next tile is whole: measured slower in the same
+// process (2.71 vs 2.47 ms, profiles/r01/ablate_compact_ab.txt), kept off
+#define WX_COMPACT_WHOLE_LOADS 0
+#endif
 #ifndef WX_SPIN_LIMIT
 #define WX_SPIN_LIMIT (1u << 20)
 #endif
@@ -310,6 +318,8 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 #define WX_DECL_TILE_IN(name, T, slot) T wx_in##slot[WX_GROUPS][4];
 #define WX_LOAD_TILE_IN(name, T, slot) \
   ::wx::load4<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4, wx_a.n_rows, wx_in##slot[wx_g]);
+#define WX_LOAD_TILE_FULL(name, T, slot) \
+  ::wx::load4_full<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4, wx_in##slot[wx_g]);
 #define WX_BIND_TILE_IN(name, T, slot) const ::wx::reg<T> name{wx_in##slot[wx_g][wx_e]};
 
 // Exclusive prefix of `tile` from its predecessors' status words; one wave.
@@ -436,6 +446,8 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
     float wx_val[WX_GROUPS][4];
     wx_u32 lane_pre[WX_GROUPS];
     // phase 1 (data): evaluate t_k, issue t_{k+1}'s loads, rank t_k
+    // (issuing each group's loads right after its evaluation measured slower:
+    // 2.72 vs 2.53 ms, profiles/r01/ablate_compact_interleave.txt)
     if (!control && have) {
 #pragma unroll
       for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
@@ -450,8 +462,11 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
         }
       }
       const wx_i64 next = tile + grid;
-      if (next < wx_a.n_tiles) {
-        const wx_i64 wx_tb = next * WX_TILE;
+      const wx_i64 wx_tb = next * WX_TILE;
+      if (WX_COMPACT_WHOLE_LOADS && WX_ALIGNED16 && wx_tb + WX_TILE <= wx_a.n_rows) {  // workgroup-uniform
+#pragma unroll
+        for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_FULL) }
+      } else if (next < wx_a.n_tiles) {
 #pragma unroll
         for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
       }
@@ -480,13 +495,48 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
       const wx_i64 excl = s_excl;
       const wx_i64 prev_base = wx_a.row_base + (tile - grid) * WX_TILE;
 #if !WX_DIAG_NO_STORE
-      for (int i = wx_dt; i < (int)prev_total; i += WX_DTHREADS) {
-        const wx_i64 pos = excl + i;
-        if (wx_a.out_val) wx::stv(wx_a.out_val + pos, s_val[i]);
+      // The tile's output run [excl, excl + total): a scalar head up to the
+      // next 32-element boundary (128 B of f32 / i32), aligned 16-byte stores
+      // of four outputs per lane, a scalar tail of < 4.  Aligned 16-B stores
+      // keep the write stream in whole lines: 6.5-7.2 TB/s for this
+      // read/write mix against 3.6-5.1 for 4-B stores (tools/bw_probe.hip).
+      const wx_i64 end = excl + (wx_i64)prev_total;
+      wx_i64 b0 = WX_COMPACT_VSTORE ? (excl + 31) & ~(wx_i64)31 : end;
+      if (b0 > end) b0 = end;
+      const wx_i64 b1 = b0 + ((end - b0) & ~(wx_i64)3);
+      const int n_head = (int)(b0 - excl), n_edge = n_head + (int)(end - b1);
+      for (int j = wx_dt; j < n_edge; j += WX_DTHREADS) {
+        const wx_i64 pos = j < n_head ? excl + j : b1 + (j - n_head);
+        const int i = (int)(pos - excl);
+        if (wx_a.out_val) wx_a.out_val[pos] = s_val[i];
         if (wx_a.out_idx) {
           const wx_i64 gi = prev_base + s_off[i];
-          if (wx_a.idx64) wx::stv(static_cast<wx_i64 *>(wx_a.out_idx) + pos, gi);
-          else wx::stv(static_cast<int *>(wx_a.out_idx) + pos, (int)gi);
+          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
+          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
+        }
+      }
+      for (wx_i64 q = b0 + 4 * (wx_i64)wx_dt; q < b1; q += 4 * (wx_i64)WX_DTHREADS) {
+        const int i = (int)(q - excl);
+        if (wx_a.out_val) {
+          typedef float v4f __attribute__((ext_vector_type(4)));
+          const v4f v = {s_val[i], s_val[i + 1], s_val[i + 2], s_val[i + 3]};
+          wx::stv(reinterpret_cast<v4f *>(wx_a.out_val + q), v);
+        }
+        if (wx_a.out_idx) {
+          if (wx_a.idx64) {
+            typedef long long v2l __attribute__((ext_vector_type(2)));
+            wx_i64 *o = static_cast<wx_i64 *>(wx_a.out_idx) + q;
+            const v2l x = {(long long)(prev_base + s_off[i]), (long long)(prev_base + s_off[i + 1])};
+            const v2l y = {(long long)(prev_base + s_off[i + 2]), (long long)(prev_base + s_off[i + 3])};
+            wx::stv(reinterpret_cast<v2l *>(o), x);
+            wx::stv(reinterpret_cast<v2l *>(o + 2), y);
+          } else {
+            typedef int v4i __attribute__((ext_vector_type(4)));
+            const unsigned base = (unsigned)prev_base;  // int32 indices: (int)(row) as the scalar path
+            const v4i x = {(int)(base + s_off[i]), (int)(base + s_off[i + 1]), (int)(base + s_off[i + 2]),
+                           (int)(base + s_off[i + 3])};
+            wx::stv(reinterpret_cast<v4i *>(static_cast<int *>(wx_a.out_idx) + q), x);
+          }
         }
       }
 #else
