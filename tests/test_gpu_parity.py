@@ -339,6 +339,38 @@ def test_group_agg_minmax_vs_oracle():
     assert g == len(rk) and np.array_equal(sums[:g].cpu().numpy(), rs)
 
 
+@pytest.mark.parametrize("minmax", [False, True])
+def test_group_many_general_keys(minmax):
+    # > 4096 distinct keys outside the LDS window: device-sorted finalize
+    n = 1_000_003
+    rng = np.random.default_rng(17)
+    keys = (rng.integers(0, 150_000, n) * 7 - 500_000).astype(np.int32)
+    in_window = rng.uniform(size=n) < 0.2
+    keys[in_window] = rng.integers(0, 2048, int(in_window.sum())).astype(np.int32)
+    cols = {"price": synth.uniform_f32(n, 1, 0.0, 40.0), "k": keys}
+    table, _ = dev_table(cols)
+    cap = 200_000
+    dk = torch.empty(cap, dtype=torch.int32, device="cuda")
+    ds = torch.empty(cap, dtype=torch.float64, device="cuda")
+    dc = torch.empty(cap, dtype=torch.int64, device="cuda")
+    dmn = torch.empty(cap, dtype=torch.float32, device="cuda")
+    dmx = torch.empty(cap, dtype=torch.float32, device="cuda")
+    for _ in range(2):  # the second call checks the tables were left clean
+        if minmax:
+            g = wx.group_agg(table, "price[idx]", "k[idx]", None, launch(), 0, cap, dk.data_ptr(), ds.data_ptr(),
+                             dc.data_ptr(), dmn.data_ptr(), dmx.data_ptr())
+            rk, rs, rc, rmn, rmx = ora.group_agg(ora.HostTable(cols), "price", "k")
+            assert np.array_equal(dmn[:g].cpu().numpy(), rmn) and np.array_equal(dmx[:g].cpu().numpy(), rmx)
+        else:
+            g = wx.group_sum(table, "price[idx]", "k[idx]", None, launch(), 0, cap, dk.data_ptr(), ds.data_ptr(),
+                             dc.data_ptr())
+            rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "k")
+        assert g == len(rk) and g > 100_000
+        assert np.array_equal(dk[:g].cpu().numpy(), rk)
+        assert np.array_equal(ds[:g].cpu().numpy(), rs)
+        assert np.array_equal(dc[:g].cpu().numpy(), rc)
+
+
 def test_group_capacity_error():
     cols = synth.c3_table(10_000)
     table, _ = dev_table(cols)

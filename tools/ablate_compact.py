@@ -48,6 +48,14 @@ VARIANTS = {
     "v0_w1": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=0,WX_COMPACT_WHOLE_LOADS=1"},
     "v1_w1": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=1"},
     "v1_w0_dw12": {"WARPDB_COMPACT_DWAVES": "12", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=0"},
+    "dw7_2pc": {"WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_BPC_FORCE": "2",
+                "WARPDB_EXTRA_DEFINES": "WX_COMPACT_MINBLOCKS=2"},
+    "dw7_1pc": {"WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_BPC_FORCE": "1"},
+    "dw7_g8_2pc": {"WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_GROUPS": "8", "WARPDB_COMPACT_BPC_FORCE": "2",
+                   "WARPDB_EXTRA_DEFINES": "WX_COMPACT_MINBLOCKS=2"},
+    "dw15": {},
+    "prof": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_PROFILE"},
+    "prof_nostore": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_PROFILE,WX_DIAG_NO_STORE"},
 }
 if len(sys.argv) > 3:
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in sys.argv[3].split(",")}

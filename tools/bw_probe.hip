@@ -213,6 +213,56 @@ __global__ __launch_bounds__(256) void r2wd4(const v4f *__restrict__ a, const v4
   }
 }
 
+// the compaction's shape step by step: 1024-thread workgroups (960 data
+// threads), a tile of G groups x 16 B per lane per column, loads of tile k+1
+// issued right after tile k is consumed, the (dense, aligned) output of tile
+// k-1 stored one iteration later, optional barriers between the phases
+template <int G, bool BAR>
+__global__ __launch_bounds__(1024) void r2wt(const v4f *__restrict__ a, const v4f *__restrict__ b,
+                                             v4f *__restrict__ ov, v4u *__restrict__ oi, size_t nq) {
+  const int t = threadIdx.x;
+  const bool data = t < 960;
+  const size_t tq = (size_t)960 * G;        // quads per tile
+  const size_t oq = tq * 5 / 8;             // output quads per tile
+  const size_t ntiles = nq / tq;
+  v4f va[G], vb[G];
+  size_t tile = blockIdx.x;
+  if (data && tile < ntiles)
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      va[g] = __builtin_nontemporal_load(a + tile * tq + g * 960 + t);
+      vb[g] = __builtin_nontemporal_load(b + tile * tq + g * 960 + t);
+    }
+  v4f keep[G];
+  bool have_prev = false;
+  size_t prev = 0;
+  for (; tile < ntiles + gridDim.x; tile += gridDim.x) {
+    const bool have = tile < ntiles;
+    if (data && have) {
+#pragma unroll
+      for (int g = 0; g < G; ++g) keep[g] = va[g] * vb[g];
+      const size_t nx = tile + gridDim.x;
+      if (nx < ntiles)
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          va[g] = __builtin_nontemporal_load(a + nx * tq + g * 960 + t);
+          vb[g] = __builtin_nontemporal_load(b + nx * tq + g * 960 + t);
+        }
+    }
+    if (BAR) __syncthreads();
+    if (data && have_prev) {
+      for (size_t k = t; k < oq; k += 960) {
+        ov[prev * oq + k] = keep[0];
+        oi[prev * oq + k] = (v4u){(unsigned)k, 1u, 2u, 3u};
+      }
+    }
+    if (BAR) __syncthreads();
+    have_prev = have;
+    prev = tile;
+    if (!have) break;
+  }
+}
+
 template <typename F>
 float time_it(F f, int reps) {
   hipEvent_t e0, e1;
@@ -258,15 +308,24 @@ int main(int argc, char **argv) {
     float ms = time_it([&] { KER<<<g, 256>>>(__VA_ARGS__); }, reps);                                          \
     printf("%-28s wg/CU %2d  %7.3f ms  %7.1f GB/s\n", name, w, ms, (double)(bytes) / ms / 1e6);               \
   }
-  RUN("read2 u4", (read2<4, false>), n * 8, (const v4f *)a, (const v4f *)b, nq, out);
   RUN("read1c u8 nt", (read1c<8, true>), n * 4, (const v4f *)a, nq, out);
-  RUN("copy u4 nt", (copy1<4, true>), n * 8, (const v4f *)a, (v4f *)ov, nq);
   RUN("r2w u4 nt", (r2w<4, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
   RUN("r2wc u8 nt", (r2wc<8, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
   RUN("r2wd u8", (r2wd<8>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+  {
+    int wp1[] = {1};
+    for (int w : wp1) {
+      float ms = time_it([&] { r2wt<4, false><<<cus * w, 1024>>>((const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq); }, reps);
+      printf("%-28s wg/CU %2d  %7.3f ms  %7.1f GB/s\n", "r2wt g4 nobar", w, ms, n * 13.0 / ms / 1e6);
+      ms = time_it([&] { r2wt<4, true><<<cus * w, 1024>>>((const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq); }, reps);
+      printf("%-28s wg/CU %2d  %7.3f ms  %7.1f GB/s\n", "r2wt g4 bar", w, ms, n * 13.0 / ms / 1e6);
+      ms = time_it([&] { r2wt<2, true><<<cus * w, 1024>>>((const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq); }, reps);
+      printf("%-28s wg/CU %2d  %7.3f ms  %7.1f GB/s\n", "r2wt g2 bar", w, ms, n * 13.0 / ms / 1e6);
+      ms = time_it([&] { r2wt<8, true><<<cus * w, 1024>>>((const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq); }, reps);
+      printf("%-28s wg/CU %2d  %7.3f ms  %7.1f GB/s\n", "r2wt g8 bar", w, ms, n * 13.0 / ms / 1e6);
+    }
+  }
   RUN("r2wd4 u8 aligned", (r2wd4<8>), n * 13, (const v4f *)a, (const v4f *)b, ov, oi, nq, 0);
-  RUN("r2wd4 u8 shift3", (r2wd4<8>), n * 13, (const v4f *)a, (const v4f *)b, ov, oi, nq, 3);
-  RUN("r2wd4 u16 shift3", (r2wd4<16>), n * 13, (const v4f *)a, (const v4f *)b, ov, oi, nq, 3);
   RUN("r2wd u16", (r2wd<16>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
   return 0;
 }

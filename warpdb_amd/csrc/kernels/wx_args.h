@@ -54,6 +54,7 @@ struct WxCompactArgs {
   wx_i64 n_tiles;
   wx_i64 row_base;
   int idx64;
+  wx_u64 *diag;  // nullable; WX_DIAG_PROFILE builds: [block][16] phase times (10 ns ticks)
 };
 
 struct WxSumArgs {
@@ -103,6 +104,17 @@ struct WxGroupFinArgs {
   wx_i64 *n_groups_out;
   wx_i64 capacity;
   int key_lo;
+  const wx_u64 *sorted;  // nullable: general-key entries pre-sorted on the device (> WX_GROUP_HSORT_MAX)
+};
+
+// General-key entries -> (key ^ sign) << 32 | used-list position, padded
+// with ~0 to npad, for the device-wide sort of a large GROUP BY.
+struct WxGroupGatherArgs {
+  const wx_u64 *ctrs;
+  const wx_u32 *h_used;
+  const wx_u64 *h_tag;
+  wx_u64 *keys;
+  wx_i64 npad;
 };
 
 struct WxTopkArgs {

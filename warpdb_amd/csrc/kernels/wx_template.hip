@@ -420,7 +420,25 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
     block_total += gsum;                                       \
   }
 
-extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCompactArgs wx_a) {
+#ifndef WX_DIAG_PROFILE
+#define WX_DIAG_PROFILE 0  // per-phase time of data wave 0 / the control wave
+#endif
+#if WX_DIAG_PROFILE
+#define WX_PT(slot)                                              \
+  do {                                                          \
+    const wx_u64 wx_now = __builtin_amdgcn_s_memrealtime();     \
+    wx_prof[slot] += wx_now - wx_prof_t;                        \
+    wx_prof_t = wx_now;                                         \
+  } while (0)
+#else
+#define WX_PT(slot) \
+  do {              \
+  } while (0)
+#endif
+#ifndef WX_COMPACT_MINBLOCKS
+#define WX_COMPACT_MINBLOCKS 1  // workgroups per CU the register budget must allow
+#endif
+extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx_project_compact(WxCompactArgs wx_a) {
   __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
   __shared__ float s_val[WX_TILE];
   __shared__ unsigned short s_off[WX_TILE];
@@ -437,6 +455,10 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
     for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
   }
   wx_u32 prev_total = 0;
+#if WX_DIAG_PROFILE
+  wx_u64 wx_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  wx_u64 wx_prof_t = __builtin_amdgcn_s_memrealtime();
+#endif
   for (int k = 0;; ++k) {
     const bool have = tile < wx_a.n_tiles;
     const bool have_prev = k > 0 && tile - grid < wx_a.n_tiles;
@@ -461,6 +483,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
           wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
         }
       }
+      WX_PT(0);  // evaluation, including the wait for t_k's loads
       const wx_i64 next = tile + grid;
       const wx_i64 wx_tb = next * WX_TILE;
       if (WX_COMPACT_WHOLE_LOADS && WX_ALIGNED16 && wx_tb + WX_TILE <= wx_a.n_rows) {  // workgroup-uniform
@@ -482,8 +505,10 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
         lane_pre[g] = pre;
         if (lane == 0) s_cnt[wave][g] = tot;
       }
+      WX_PT(1);  // issue t_{k+1} loads + rank
     }
     __syncthreads();
+    WX_PT(2);  // barrier 1
     // phase 2: control publishes t_k's aggregate; data waves write t_{k-1} out of LDS
     wx_u32 block_total = 0;
     wx_u32 grp_base[WX_GROUPS];
@@ -543,7 +568,9 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
       if (excl == -1 && wx_a.out_val) wx_a.out_val[0] = s_val[wx_dt];
 #endif
     }
+    WX_PT(3);  // data: stores of t_{k-1}; control: publish
     __syncthreads();
+    WX_PT(4);  // barrier 2
     // phase 3: data waves stage t_k; the control wave resolves t_k's offset
     // (overlapping the staging and phase 1 of the next iteration)
     if (control) {
@@ -576,9 +603,16 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK) void wx_project_compact(WxCom
         }
       }
     }
+    WX_PT(5);  // data: LDS staging of t_k; control: look-back
     prev_total = block_total;
     tile += grid;
   }
+#if WX_DIAG_PROFILE
+  if (wx_a.diag && (tid == 0 || tid == WX_DTHREADS)) {
+    wx_u64 *d = wx_a.diag + (wx_u64)blockIdx.x * 16 + (tid == 0 ? 0 : 8);
+    for (int i = 0; i < 6; ++i) d[i] = wx_prof[i];
+  }
+#endif
 }
 
 // One tile per workgroup, taken from a ticket counter (robust fallback).
@@ -891,23 +925,37 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs 
 // to the accumulators the atomics left beyond L2), ranked by one block scan.
 #define WX_GFIN_BLOCK 1024
 static_assert(WX_GWIN == 2 * WX_GFIN_BLOCK, "two window bins per finalize thread");
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_gather(WxGroupGatherArgs a) {
+  const wx_i64 nh = (wx_i64)a.ctrs[0];
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.npad; i += (wx_i64)gridDim.x * WX_BLOCK) {
+    wx_u64 e = ~0ull;
+    if (i < nh) {
+      const wx_u32 key = (wx_u32)a.h_tag[a.h_used[i]];
+      e = ((wx_u64)(key ^ 0x80000000u) << 32) | (wx_u32)i;
+    }
+    a.keys[i] = e;
+  }
+}
+
 extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(WxGroupFinArgs a) {
   __shared__ wx_u64 s_ent[WX_HSORT_MAX];  // (key ^ sign) << 32 | used-list position
   __shared__ wx_u32 s_wtot[WX_GFIN_BLOCK / 64];
   __shared__ wx_i64 s_nlo;
   const int tid = threadIdx.x;
   const wx_i64 n_hash = (wx_i64)a.ctrs[0];
-  const bool too_many = n_hash > WX_HSORT_MAX;
+  const bool presorted = a.sorted != nullptr;
+  const bool too_many = n_hash > WX_HSORT_MAX && !presorted;
   if (too_many) {
     if (tid == 0) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_UNSUPPORTED);
   }
-  const int nh = too_many ? 0 : (int)n_hash;
+  const wx_i64 nh = too_many ? 0 : n_hash;
   int npad = 1;
-  while (npad < nh) npad <<= 1;
+  while (!presorted && npad < nh) npad <<= 1;
+#define WX_ENT(i) (presorted ? a.sorted[(i)] : s_ent[(i)])
   // window bins of this thread, loaded before the (rare) hash-key sort
   const int b0 = tid * 2;
   const wx_u64 wc0 = a.win_cnt[b0], wc1 = a.win_cnt[b0 + 1];
-  for (int i = tid; i < npad; i += WX_GFIN_BLOCK) {
+  for (int i = tid; !presorted && i < npad; i += WX_GFIN_BLOCK) {
     wx_u64 e = ~0ull;
     if (i < nh) {
       const wx_u32 slot = a.h_used[i];
@@ -917,7 +965,7 @@ extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(Wx
     s_ent[i] = e;
   }
   __syncthreads();
-  for (int k = 2; k <= npad; k <<= 1)
+  for (int k = 2; !presorted && k <= npad; k <<= 1)
     for (int j = k >> 1; j > 0; j >>= 1) {
       for (int i = tid; i < npad; i += WX_GFIN_BLOCK) {
         const int p = i ^ j;
@@ -929,11 +977,15 @@ extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(Wx
       }
       __syncthreads();
     }
-  // number of hash keys below the window
+  // number of hash keys below the window (binary search in key order)
   if (tid == 0) {
-    wx_i64 c = 0;
-    while (c < nh && (int)((wx_u32)(s_ent[c] >> 32) ^ 0x80000000u) < a.key_lo) ++c;
-    s_nlo = c;
+    wx_i64 lo = 0, hi = nh;
+    while (lo < hi) {
+      const wx_i64 mid = (lo + hi) >> 1;
+      if ((int)((wx_u32)(WX_ENT(mid) >> 32) ^ 0x80000000u) < a.key_lo) lo = mid + 1;
+      else hi = mid;
+    }
+    s_nlo = lo;
   }
   __syncthreads();
   const wx_i64 nlo = s_nlo;
@@ -982,10 +1034,10 @@ extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(Wx
   }
   const wx_i64 out_pos = nlo + wsum;
   // hash entries: below-window ones first, the rest after the window
-  for (int i = tid; i < nh; i += WX_GFIN_BLOCK) {
-    const wx_u64 e = s_ent[i];
+  for (wx_i64 i = tid; i < nh; i += WX_GFIN_BLOCK) {
+    const wx_u64 e = WX_ENT(i);
     const wx_u32 slot = a.h_used[(wx_u32)e];
-    const wx_i64 pos = (i < nlo) ? (wx_i64)i : out_pos + (i - nlo);
+    const wx_i64 pos = (i < nlo) ? i : out_pos + (i - nlo);
     if (pos < a.capacity) {
       a.out_keys[pos] = (int)((wx_u32)(e >> 32) ^ 0x80000000u);
       a.out_sums[pos] = a.h_sum[slot];
@@ -1014,6 +1066,7 @@ extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(Wx
     *a.n_groups_out = too_many ? -1 : total;
     if (total > a.capacity) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_CAPACITY);
   }
+#undef WX_ENT
 }
 #endif
 
