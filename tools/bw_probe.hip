@@ -175,11 +175,14 @@ __global__ __launch_bounds__(256) void r2wd(const v4f *__restrict__ a, const v4f
       va[u] = __builtin_nontemporal_load(a + i);
       vb[u] = __builtin_nontemporal_load(b + i);
     }
+    v4f acc = va[0] * vb[0];
+#pragma unroll
+    for (int u = 1; u < U; ++u) acc += va[u] * vb[u];  // every load stays live
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t k = u * 256 + threadIdx.x;
       if (k < ospan) {
-        ov[ob + k] = va[u] * vb[u];
+        ov[ob + k] = acc;
         oi[ob + k] = (v4u){(unsigned)k, (unsigned)k + 1, (unsigned)k + 2, (unsigned)k + 3};
       }
     }
@@ -250,9 +253,12 @@ __global__ __launch_bounds__(1024) void r2wt(const v4f *__restrict__ a, const v4
         }
     }
     if (BAR) __syncthreads();
+    v4f acc = keep[0];
+#pragma unroll
+    for (int g = 1; g < G; ++g) acc += keep[g];  // every group's loads stay live
     if (data && have_prev) {
       for (size_t k = t; k < oq; k += 960) {
-        ov[prev * oq + k] = keep[0];
+        ov[prev * oq + k] = acc;
         oi[prev * oq + k] = (v4u){(unsigned)k, 1u, 2u, 3u};
       }
     }
@@ -309,8 +315,6 @@ int main(int argc, char **argv) {
     printf("%-28s wg/CU %2d  %7.3f ms  %7.1f GB/s\n", name, w, ms, (double)(bytes) / ms / 1e6);               \
   }
   RUN("read1c u8 nt", (read1c<8, true>), n * 4, (const v4f *)a, nq, out);
-  RUN("r2w u4 nt", (r2w<4, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
-  RUN("r2wc u8 nt", (r2wc<8, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
   RUN("r2wd u8", (r2wd<8>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
   {
     int wp1[] = {1};
@@ -325,7 +329,5 @@ int main(int argc, char **argv) {
       printf("%-28s wg/CU %2d  %7.3f ms  %7.1f GB/s\n", "r2wt g8 bar", w, ms, n * 13.0 / ms / 1e6);
     }
   }
-  RUN("r2wd4 u8 aligned", (r2wd4<8>), n * 13, (const v4f *)a, (const v4f *)b, ov, oi, nq, 0);
-  RUN("r2wd u16", (r2wd<16>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
   return 0;
 }

@@ -522,9 +522,10 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #if !WX_DIAG_NO_STORE
       // The tile's output run [excl, excl + total): a scalar head up to the
       // next 32-element boundary (128 B of f32 / i32), aligned 16-byte stores
-      // of four outputs per lane, a scalar tail of < 4.  Aligned 16-B stores
-      // keep the write stream in whole lines: 6.5-7.2 TB/s for this
-      // read/write mix against 3.6-5.1 for 4-B stores (tools/bw_probe.hip).
+      // of four outputs per lane, a scalar tail of < 4.  For this kernel's
+      // 8 B read + 5 B write mix the probe gives 6.2 TB/s with aligned 16-B
+      // stores (r2wt) against 5.1-5.4 with 4-B stores (r2wd4) and 3.6 with
+      // 4-B stores off a 16-B boundary (tools/bw_probe.hip).
       const wx_i64 end = excl + (wx_i64)prev_total;
       wx_i64 b0 = WX_COMPACT_VSTORE ? (excl + 31) & ~(wx_i64)31 : end;
       if (b0 > end) b0 = end;
