@@ -200,6 +200,7 @@ def main():
     else:
         bytes_per_launch = n * 8
     achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
+    read_bytes = n * (4 if args.workload in ("sum", "topk") else 8)
 
     total_rows = n * world * args.steps
     value = total_rows / elapsed
@@ -238,7 +239,10 @@ def main():
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                          "kernel": kname, "kernel_ms": round(kern_avg_ms, 4),
-                         "bytes_per_launch": bytes_per_launch},
+                         "bytes_per_launch": bytes_per_launch,
+                         # BASELINE.md's "HBM-read roofline": input bytes only (8 B/row for
+                         # project / group, 4 B/row for sum / top-K) over the same time
+                         "read_only_frac": round(read_bytes / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
             "cpu_baseline": cpu,
         }
         if passing is not None:
