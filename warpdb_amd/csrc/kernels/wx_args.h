@@ -34,6 +34,8 @@ typedef unsigned int wx_u32;
 #define WX_GROUP_WINDOW 2048
 #define WX_GROUP_HSORT_MAX 4096
 #define WX_TOPK_MAX 32
+#define WX_TOPK_SLOTS 64        // top-K grid-wide bound: one slot per wave lane
+#define WX_TOPK_SLOT_STRIDE 64  // u32 elements between slots (256 B)
 #define WX_SORT_LDS (WX_BLOCK * 8)
 
 struct WxDenseArgs {
@@ -119,8 +121,9 @@ struct WxGroupGatherArgs {
 
 struct WxTopkArgs {
   const void *col[WX_MAX_COLS];
-  wx_u32 *cand_k;  // [gridDim.x * K]
-  wx_i64 *cand_i;  // [gridDim.x * K]
+  wx_u32 *cand_k;    // [gridDim.x * K]
+  wx_i64 *cand_i;    // [gridDim.x * K]
+  wx_u32 *g_thresh;  // [WX_TOPK_SLOTS * WX_TOPK_SLOT_STRIDE] lower bounds on the K-th best rank (0 = none), zeroed per call
   wx_i64 n_rows;
 };
 

@@ -1204,8 +1204,21 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
   // keys against the worst (rows failing the WHERE count as -inf/+inf; NaN
   // keys never enter a full list; ties never enter, later rows lose): only
   // batches that can change the list re-evaluate their rows and insert.
+  // Thresholds: the K-th best key of any set of rows is a lower bound on the
+  // global K-th best, so rows strictly worse can be dropped.  After a batch in
+  // which a lane inserted, the wave takes the exact K-th best over all its
+  // lanes' lists (K rounds of a wave arg-max; the max over lanes of each
+  // lane's own K-th best is far weaker with ≈1 900 rows per lane) and raises
+  // the grid-wide bound with atomicMax on the order-preserving rank.  The
+  // bound lives in WX_TOPK_SLOTS slots on separate 256-B lines (a single
+  // address serialised ≈50K early atomics: 2.4 ms); a wave publishes to its
+  // workgroup's slot and every 8th batch reads all slots with one vector load
+  // (lane l: slot l) and a wave max (relaxed: a stale value is still a bound).
   const float wx_none = WX_TOPK_DESC ? -__builtin_inff() : __builtin_inff();
-  float wx_T = wx_none;  // wave threshold: best worst-key over the wave's full lanes
+  float wx_T = wx_none;   // best known bound (this wave and the grid)
+  wx_u32 wx_pub = 0u;     // best rank this wave has found
+  wx_u32 wx_gseen = 0u;   // best grid-wide rank this wave has seen or published
+  int wx_batch = 0;
   const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
   const wx_i64 wx_nfull = wx_a.n_rows >> 2;
   for (wx_i64 wx_base = (wx_i64)blockIdx.x * WX_SPAN; wx_base < wx_nq; wx_base += (wx_i64)gridDim.x * WX_SPAN) {
@@ -1224,11 +1237,25 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
         WX_COLS(WX_LOAD_U)
       }
     }
-    bool wx_slow = !wx_whole || !wx_L.full || wx_L.wf != wx_L.wf;
+    if ((wx_batch++ & 7) == 7) {
+      wx_u32 wx_g = __hip_atomic_load(wx_a.g_thresh + (threadIdx.x & 63) * WX_TOPK_SLOT_STRIDE, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) {
+        const wx_u32 x = __shfl_xor(wx_g, o);
+        wx_g = x > wx_g ? x : wx_g;
+      }
+      if (wx_g > wx_gseen) {
+        wx_gseen = wx_g;
+        const float gf = wx::key_of(wx_g);
+        wx_T = WX_TOPK_DESC ? fmaxf(wx_T, gf) : fminf(wx_T, gf);
+      }
+    }
+    bool wx_slow = !wx_whole;
     if (!wx_slow) {
-      // wx_T >= this lane's worst: rows strictly worse than T cannot reach the
-      // top K (T is the K-th best of another lane's rows); rows equal to T may
-      // (smaller index), and rows equal to the lane's own worst may not.
+      // Rows strictly worse than T cannot reach the top K; rows equal to T may
+      // (smaller index).  A full lane also needs a row strictly better than its
+      // own worst (its rows arrive in increasing index order).
       float wx_m = wx_none;
 #pragma unroll
       for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
@@ -1241,9 +1268,10 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
           wx_m = WX_TOPK_DESC ? fmaxf(wx_m, wx_v) : fminf(wx_m, wx_v);
         }
       }
-      const bool wx_tie_ok = WX_TOPK_DESC ? (wx_T > wx_L.wf) : (wx_T < wx_L.wf);
-      wx_slow = WX_TOPK_DESC ? (wx_tie_ok ? wx_m >= wx_T : wx_m > wx_L.wf)
-                             : (wx_tie_ok ? wx_m <= wx_T : wx_m < wx_L.wf);
+      const bool wx_beats_T = wx_T == wx_none || (WX_TOPK_DESC ? wx_m >= wx_T : wx_m <= wx_T);
+      const bool wx_beats_own =
+          !wx_L.full || wx_L.wf != wx_L.wf || (WX_TOPK_DESC ? wx_m > wx_L.wf : wx_m < wx_L.wf);
+      wx_slow = wx_beats_T && wx_beats_own;
     }
     if (wx_slow) {
 #pragma unroll
@@ -1261,15 +1289,25 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
         }
       }
     }
-    // refresh the wave threshold after any insert in the wave
+    // after any insert in the wave: the wave's exact K-th best
     if (__builtin_amdgcn_ballot_w64(wx_slow)) {
-      float t = (wx_L.full && wx_L.wf == wx_L.wf) ? wx_L.wf : wx_none;
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) {
-        const float x = __shfl_xor(t, o);
-        t = WX_TOPK_DESC ? fmaxf(t, x) : fminf(t, x);
+      wx::TopList wx_c = wx_L;
+      wx_u32 wk[WX_TOPK_K];
+      wx_i64 wi[WX_TOPK_K];
+      wx::wave_merge(wx_c, wk, wi);
+      const wx_u32 r = wi[WX_TOPK_K - 1] != WX_IDX_NONE ? wk[WX_TOPK_K - 1] : 0u;  // 0: fewer than K rows, or NaN
+      if (r > wx_pub) {
+        const float t = wx::key_of(r);
+        wx_T = WX_TOPK_DESC ? fmaxf(wx_T, t) : fminf(wx_T, t);
+        wx_pub = r;
+        // publish only what beats the grid's bound as last seen: one address
+        // taking an atomic from every wave on every improvement serialises
+        if (r > wx_gseen) {
+          if ((threadIdx.x & 63) == 0)
+            atomicMax(wx_a.g_thresh + (blockIdx.x % WX_TOPK_SLOTS) * WX_TOPK_SLOT_STRIDE, r);
+          wx_gseen = r;
+        }
       }
-      wx_T = t;
     }
   }
   wx_u32 bk[WX_TOPK_K];
