@@ -96,9 +96,33 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    # RCCL over xGMI, one GPU per rank.  WARPDB_DIST_BACKEND=gloo lets several
+    # ranks share one GPU (rehearsal of the multi-rank path on a 1-GPU box);
+    # its exchanges go through host tensors.
+    backend = os.environ.get("WARPDB_DIST_BACKEND", "nccl")
+    local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "gloo":
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    def all_gather(out, inp):
+        if backend == "gloo":
+            parts = [torch.empty_like(inp, device="cpu") for _ in range(world)]
+            dist.all_gather(parts, inp.cpu())
+            out.copy_(torch.cat(parts))
+        else:
+            dist.all_gather_into_tensor(out, inp)
+
+    def all_reduce(t, op=dist.ReduceOp.SUM):
+        if backend == "gloo":
+            h = t.cpu()
+            dist.all_reduce(h, op=op)
+            t.copy_(h)
+        else:
+            dist.all_reduce(t, op=op)
 
     def barrier():
         if world > 1:
@@ -133,7 +157,7 @@ def main():
             wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", Lx, wx.MODE_COMPACT,
                               out_v.data_ptr(), out_i.data_ptr(), 4, 0, d_count=counts.data_ptr())
             if world > 1:  # global placement of each shard's rows
-                dist.all_gather_into_tensor(gathered, counts)
+                all_gather(gathered, counts)
     elif args.workload == "sum":
         res = torch.zeros(2, dtype=torch.float64, device="cuda")
 
@@ -141,7 +165,7 @@ def main():
             wx.reduce_sum(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", Lx, d_out=res.data_ptr(),
                           want_host=False)
             if world > 1:
-                dist.all_reduce(res[:1])
+                all_reduce(res[:1])
     elif args.workload == "group":
         cap = 4096
         keys = torch.empty(cap, dtype=torch.int32, device="cuda")
@@ -153,7 +177,7 @@ def main():
             wx.group_sum(table, "price[idx]", "quantity[idx]", None, Lx, 0, cap, keys.data_ptr(), sums.data_ptr(),
                          cnts.data_ptr(), d_n_groups=ng.data_ptr(), want_count=False)
             if world > 1:  # dense 1K-bin partials: keys are identical on every shard
-                dist.all_reduce(sums[:1024])
+                all_reduce(sums[:1024])
     else:
         tk = torch.empty(5, dtype=torch.float32, device="cuda")
         ti = torch.empty(5, dtype=torch.int64, device="cuda")
@@ -164,7 +188,7 @@ def main():
             wx.topk(table, "price[idx]", None, "discount(price[idx], 0.9f)", 5, True, Lx, tk.data_ptr(),
                     ti.data_ptr(), tv.data_ptr(), row_base=row_base, d_count=counts.data_ptr(), want_count=False)
             if world > 1:
-                dist.all_gather_into_tensor(allk, tk)
+                all_gather(allk, tk)
 
     for _ in range(args.warmup):
         step(L)
@@ -183,10 +207,10 @@ def main():
     wx.check(L)
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = t.item()
         km = torch.tensor([kern_ms / max(1, launches)], dtype=torch.float64, device="cuda")
-        dist.all_reduce(km, op=dist.ReduceOp.MAX)
+        all_reduce(km, op=dist.ReduceOp.MAX)
         kern_avg_ms = km.item()
     else:
         kern_avg_ms = kern_ms / max(1, launches)
