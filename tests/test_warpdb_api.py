@@ -186,3 +186,26 @@ def test_sharded_query_single_rank():
     rk3, rs3, rc3 = ora.group_sum(ora.HostTable(cols3), "price", "quantity")
     assert np.array_equal(gk.cpu().numpy(), rk3) and np.array_equal(gs.cpu().numpy(), rs3)
     dist.destroy_process_group()
+
+
+def test_bench_two_ranks_on_one_gpu():
+    # the multi-rank bench path (torchrun rendezvous, shards, exchanges, max-over-
+    # ranks timing) with two ranks sharing the GPU over gloo; RCCL on the 8-GPU node
+    import json
+    import socket
+    import sys
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = dict(os.environ, WARPDB_DIST_BACKEND="gloo")
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", "2", "--rows", "1e7", "--steps", "3", "--warmup", "1"],
+                       capture_output=True, text=True, cwd=ROOT, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = lines[0]
+    assert d["n_gpus"] == 2 and d["config"]["total_rows"] == 2 * 10**7 and d["value"] > 0
+    assert d["config"]["passing_rows_per_gpu"] > 0.6 * 10**7

@@ -54,6 +54,7 @@ VARIANTS = {
     "dw7_g8_2pc": {"WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_GROUPS": "8", "WARPDB_COMPACT_BPC_FORCE": "2",
                    "WARPDB_EXTRA_DEFINES": "WX_COMPACT_MINBLOCKS=2"},
     "dw15": {},
+    "static_sched": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_TICKETS=0"},
     "prof": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_PROFILE"},
     "prof_nostore": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_PROFILE,WX_DIAG_NO_STORE"},
 }

@@ -435,6 +435,13 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
   do {              \
   } while (0)
 #endif
+#ifndef WX_COMPACT_TICKETS
+// Tiles from an atomic ticket counter (two iterations ahead) instead of the
+// static b, b + grid, ... schedule: a tile is only ever taken by a running
+// workgroup, so the look-back progresses whatever else shares the GPU (the
+// static schedule deadlocked when two processes' compactions overlapped).
+#define WX_COMPACT_TICKETS 1
+#endif
 #ifndef WX_COMPACT_MINBLOCKS
 #define WX_COMPACT_MINBLOCKS 1  // workgroups per CU the register budget must allow
 #endif
@@ -443,11 +450,22 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
   __shared__ float s_val[WX_TILE];
   __shared__ unsigned short s_off[WX_TILE];
   __shared__ wx_i64 s_excl;
+  __shared__ wx_i64 s_tiles[4];  // ticket ring: slot k & 3 holds iteration k's tile
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool control = wave == WX_DWAVES;
   const int wx_dt = tid;  // data-thread index (data waves only)
   const wx_i64 grid = gridDim.x;
+#if WX_COMPACT_TICKETS
+  if (tid == 0) {
+    s_tiles[0] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tiles[1] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  wx_i64 tile = s_tiles[0];
+#else
   wx_i64 tile = blockIdx.x;
+#endif
+  wx_i64 prev_tile = -1;
   WX_COLS(WX_DECL_TILE_IN)
   if (!control && tile < wx_a.n_tiles) {
     const wx_i64 wx_tb = tile * WX_TILE;
@@ -461,8 +479,13 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #endif
   for (int k = 0;; ++k) {
     const bool have = tile < wx_a.n_tiles;
-    const bool have_prev = k > 0 && tile - grid < wx_a.n_tiles;
+    const bool have_prev = k > 0 && prev_tile < wx_a.n_tiles;
     if (!have && !have_prev) break;
+#if WX_COMPACT_TICKETS
+    const wx_i64 next_tile = s_tiles[(k + 1) & 3];  // fetched two iterations ahead
+#else
+    const wx_i64 next_tile = tile + grid;
+#endif
     const wx_i64 tile_base = tile * WX_TILE;
     bool wx_keep[WX_GROUPS][4];
     float wx_val[WX_GROUPS][4];
@@ -484,7 +507,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
         }
       }
       WX_PT(0);  // evaluation, including the wait for t_k's loads
-      const wx_i64 next = tile + grid;
+      const wx_i64 next = next_tile;
       const wx_i64 wx_tb = next * WX_TILE;
       if (WX_COMPACT_WHOLE_LOADS && WX_ALIGNED16 && wx_tb + WX_TILE <= wx_a.n_rows) {  // workgroup-uniform
 #pragma unroll
@@ -516,9 +539,17 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     if (control) {
       if (have && lane == 0)
         wx::st_agent(&wx_a.status[tile], (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
+#if WX_COMPACT_TICKETS
+      // the tile of iteration k + 2 (slot last read as `prev` in iteration k - 1)
+      if (lane == 0)
+        s_tiles[(k + 2) & 3] = next_tile < wx_a.n_tiles
+                                   ? (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                   : wx_a.n_tiles;  // past the end: stop taking tickets
+#endif
     } else if (have_prev) {
       const wx_i64 excl = s_excl;
-      const wx_i64 prev_base = wx_a.row_base + (tile - grid) * WX_TILE;
+      const wx_i64 prev_base = wx_a.row_base + prev_tile * WX_TILE;
 #if !WX_DIAG_NO_STORE
       // The tile's output run [excl, excl + total): a scalar head up to the
       // next 32-element boundary (128 B of f32 / i32), aligned 16-byte stores
@@ -606,7 +637,8 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     }
     WX_PT(5);  // data: LDS staging of t_k; control: look-back
     prev_total = block_total;
-    tile += grid;
+    prev_tile = tile;
+    tile = next_tile;
   }
 #if WX_DIAG_PROFILE
   if (wx_a.diag && (tid == 0 || tid == WX_DTHREADS)) {
