@@ -487,7 +487,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     const wx_i64 next_tile = tile + grid;
 #endif
     const wx_i64 tile_base = tile * WX_TILE;
-    bool wx_keep[WX_GROUPS][4];
+    wx_u32 wx_kb = 0;  // bit 4g + e: row (g, e) passes (a VGPR, not 16 SGPR-pair lane masks)
     float wx_val[WX_GROUPS][4];
     wx_u32 lane_pre[WX_GROUPS];
     // phase 1 (data): evaluate t_k, issue t_{k+1}'s loads, rank t_k
@@ -502,7 +502,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
           const wx_i64 idx = tile_base + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4 + wx_e;
           bool wx_k = idx < wx_a.n_rows;
           wx_k = wx_k && WX_EVAL_COND();
-          wx_keep[wx_g][wx_e] = wx_k;
+          wx_kb |= (wx_k ? 1u : 0u) << (wx_g * 4 + wx_e);
           wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
         }
       }
@@ -521,7 +521,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
         wx_u32 pre = 0, tot = 0;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const wx_u64 m = __builtin_amdgcn_ballot_w64(wx_keep[g][e]);
+          const wx_u64 m = __builtin_amdgcn_ballot_w64(((wx_kb >> (g * 4 + e)) & 1u) != 0u);
           pre += wx::lanes_below(m);
           tot += (wx_u32)__builtin_popcountll(m);
         }
@@ -627,7 +627,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
         wx_u32 pos = grp_base[g] + lane_pre[g];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          if (wx_keep[g][e]) {
+          if ((wx_kb >> (g * 4 + e)) & 1u) {
             s_val[pos] = wx_val[g][e];
             s_off[pos] = (unsigned short)(g * (WX_DTHREADS * 4) + wx_dt * 4 + e);
             ++pos;
