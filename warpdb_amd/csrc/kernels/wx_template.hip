@@ -494,13 +494,17 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     // (issuing each group's loads right after its evaluation measured slower:
     // 2.72 vs 2.53 ms, profiles/r01/ablate_compact_interleave.txt)
     if (!control && have) {
+      // rows of this tile inside the table (workgroup-uniform, 32-bit)
+      const wx_u32 wx_rows = (wx_u32)(wx_a.n_rows - tile_base < WX_TILE ? wx_a.n_rows - tile_base : WX_TILE);
 #pragma unroll
       for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
 #pragma unroll
         for (int wx_e = 0; wx_e < 4; ++wx_e) {
           WX_COLS(WX_BIND_TILE_IN)
-          const wx_i64 idx = tile_base + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4 + wx_e;
-          bool wx_k = idx < wx_a.n_rows;
+          const wx_u32 wx_lrow = (wx_u32)(wx_g * (WX_DTHREADS * 4) + wx_dt * 4 + wx_e);
+          const wx_i64 idx = tile_base + wx_lrow;  // dead unless the expression names idx
+          (void)idx;
+          bool wx_k = wx_lrow < wx_rows;
           wx_k = wx_k && WX_EVAL_COND();
           wx_kb |= (wx_k ? 1u : 0u) << (wx_g * 4 + wx_e);
           wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
