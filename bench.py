@@ -146,6 +146,8 @@ def main():
         qdt = wx.FLOAT32
     table = wx.Table(n, [wx.Column("price", wx.FLOAT32, price.data_ptr()), wx.Column("quantity", qdt, qty.data_ptr())])
     query, kname = WORKLOADS[args.workload]
+    if args.workload == "project" and os.environ.get("WARPDB_COMPACT_SCHED", "deep") == "deep":
+        kname = "wx_project_compact_deep"
     counts = torch.zeros(1, dtype=torch.int64, device="cuda")
     gathered = torch.zeros(world, dtype=torch.int64, device="cuda")
 

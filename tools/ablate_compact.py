@@ -32,31 +32,42 @@ cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
 ref_count = int((price > 15.0).sum().item())
 
 VARIANTS = {
-    "dw8_g4": {},
-    "dw12_g4": {"WARPDB_COMPACT_DWAVES": "12"},
-    "dw15_g4": {"WARPDB_COMPACT_DWAVES": "15"},
-    "dw12_g6": {"WARPDB_COMPACT_DWAVES": "12", "WARPDB_COMPACT_GROUPS": "6"},
-    "dw15_g4_lb2": {"WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=2"},
-    "dw15_nolookback": {"WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK"},
-    "dw15_nostore": {"WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_STORE"},
-    "dw15_plainld": {"WARPDB_EXTRA_DEFINES": "WX_NT_LOAD=0"},
-    "dw15_ntst": {"WARPDB_EXTRA_DEFINES": "WX_NT_STORE=1"},
-    "dw15_plainld_ntst": {"WARPDB_EXTRA_DEFINES": "WX_NT_LOAD=0,WX_NT_STORE=1"},
-    "dw12_ntst": {"WARPDB_COMPACT_DWAVES": "12", "WARPDB_EXTRA_DEFINES": "WX_NT_STORE=1"},
-    "v0_w0": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=0,WX_COMPACT_WHOLE_LOADS=0"},
-    "v1_w0": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=0"},
-    "v0_w1": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=0,WX_COMPACT_WHOLE_LOADS=1"},
-    "v1_w1": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=1"},
-    "v1_w0_dw12": {"WARPDB_COMPACT_DWAVES": "12", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=0"},
-    "dw7_2pc": {"WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_BPC_FORCE": "2",
+    "dw8_g4": {"WARPDB_COMPACT_SCHED": "static"},
+    "dw12_g4": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "12"},
+    "dw15_g4": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "15"},
+    "dw12_g6": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "12", "WARPDB_COMPACT_GROUPS": "6"},
+    "dw15_g4_lb2": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "15", "WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=2"},
+    "dw15_nolookback": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "15",
+                        "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK"},
+    "dw15_nostore": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "15",
+                     "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_STORE"},
+    "dw15_plainld": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_NT_LOAD=0"},
+    "dw15_ntst": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_NT_STORE=1"},
+    "dw15_plainld_ntst": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_NT_LOAD=0,WX_NT_STORE=1"},
+    "dw12_ntst": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "12", "WARPDB_EXTRA_DEFINES": "WX_NT_STORE=1"},
+    "v0_w0": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=0,WX_COMPACT_WHOLE_LOADS=0"},
+    "v1_w0": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=0"},
+    "v0_w1": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=0,WX_COMPACT_WHOLE_LOADS=1"},
+    "v1_w1": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=1"},
+    "v1_w0_dw12": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "12", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_VSTORE=1,WX_COMPACT_WHOLE_LOADS=0"},
+    "dw7_2pc": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_BPC_FORCE": "2",
                 "WARPDB_EXTRA_DEFINES": "WX_COMPACT_MINBLOCKS=2"},
-    "dw7_1pc": {"WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_BPC_FORCE": "1"},
-    "dw7_g8_2pc": {"WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_GROUPS": "8", "WARPDB_COMPACT_BPC_FORCE": "2",
+    "dw7_1pc": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_BPC_FORCE": "1"},
+    "dw7_g8_2pc": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "7", "WARPDB_COMPACT_GROUPS": "8", "WARPDB_COMPACT_BPC_FORCE": "2",
                    "WARPDB_EXTRA_DEFINES": "WX_COMPACT_MINBLOCKS=2"},
-    "dw15": {},
-    "static_sched": {"WARPDB_EXTRA_DEFINES": "WX_COMPACT_TICKETS=0"},
-    "prof": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_PROFILE"},
-    "prof_nostore": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_PROFILE,WX_DIAG_NO_STORE"},
+    "dw15": {"WARPDB_COMPACT_SCHED": "static"},
+    "deep": {},
+    "static_sched": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_TICKETS=0"},
+    "nolb_unaligned": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK=2"},
+    "deep_dw12": {"WARPDB_COMPACT_SCHED": "deep", "WARPDB_COMPACT_DWAVES": "12"},
+    "deep_dw15_g3": {"WARPDB_COMPACT_SCHED": "deep", "WARPDB_COMPACT_GROUPS": "3"},
+    "dw12": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "12"},
+    "lb_sleep0": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_LB_SLEEP=0"},
+    "lb_sleep1": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_LB_SLEEP=1"},
+    "lb_sleep6": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_LB_SLEEP=6"},
+    "lb_lanes2": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_LB_PER_LANE=2"},
+    "prof": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_DIAG_PROFILE"},
+    "prof_nostore": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_DIAG_PROFILE,WX_DIAG_NO_STORE"},
 }
 if len(sys.argv) > 3:
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in sys.argv[3].split(",")}

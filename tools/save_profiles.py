@@ -22,7 +22,9 @@ for w in wls:
     b = [json.loads(line) for line in open(os.path.join(go, "refresh", f"bench_{w}.log")) if line.startswith("{")][0]
     pmc_sum = os.path.join(go, f"pmc_{w}", "summary.json")
     if os.path.exists(pmc_sum):
-        s = json.load(open(pmc_sum))[k]
+        s = json.load(open(pmc_sum))
+        k = b["roofline"]["kernel"] if b["roofline"]["kernel"] in s else k
+        s = s[k]
         d = {"kernel": k, "rows": b["config"]["rows_per_gpu"],
              "source": f"rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes (tools/pmc_run.sh {w}), {rnd}",
              "fetch_size_kb_avg": s["FETCH_SIZE"]["avg"], "write_size_kb_avg": s["WRITE_SIZE"]["avg"],

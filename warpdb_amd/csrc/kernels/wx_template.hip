@@ -613,7 +613,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
       if (have) {
         wx_i64 excl = 0;
 #if WX_DIAG_NO_LOOKBACK
-        excl = tile_base / 2;  // diagnostic build: timing only, results invalid
+        excl = WX_DIAG_NO_LOOKBACK == 2 ? tile_base * 5 / 8 + 3 : tile_base / 2;  // diagnostic: timing only
 #else
         if (tile > 0) {
           excl = wx_lookback(wx_a, tile);
@@ -651,6 +651,180 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
   }
 #endif
 }
+
+// Deeper pipeline (WARPDB_COMPACT_SCHED=deep): tile t_j is evaluated and
+// staged in iteration j, its offset resolved by the control wave in
+// iteration j + 1 (its predecessors' aggregates have long landed), and its
+// output written in iteration j + 2 — the look-back gets a whole iteration
+// of slack instead of half of one.  Two stage buffers (2 x 6 B per tile row),
+// so only compiled when selected.
+#if defined(WX_COMPACT_STATIC) && WX_COMPACT_STATIC == 3
+extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx_project_compact_deep(WxCompactArgs wx_a) {
+  __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
+  __shared__ float s_val[2][WX_TILE];
+  __shared__ unsigned short s_off[2][WX_TILE];
+  __shared__ wx_i64 s_excl[2];
+  __shared__ wx_i64 s_tiles[4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool control = wave == WX_DWAVES;
+  const int wx_dt = tid;
+  if (tid == 0) {
+    s_tiles[0] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tiles[1] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  wx_i64 tile = s_tiles[0];
+  wx_i64 tile1 = -1, tile2 = -1;   // tiles of iterations k - 1 and k - 2
+  wx_u32 tot1 = 0, tot2 = 0;       // their passing counts
+  WX_COLS(WX_DECL_TILE_IN)
+  if (!control && tile < wx_a.n_tiles) {
+    const wx_i64 wx_tb = tile * WX_TILE;
+#pragma unroll
+    for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
+  }
+  for (int k = 0;; ++k) {
+    const bool have = tile < wx_a.n_tiles;
+    const bool have1 = k >= 1 && tile1 < wx_a.n_tiles;
+    const bool have2 = k >= 2 && tile2 < wx_a.n_tiles;
+    if (!have && !have1 && !have2) break;
+    const wx_i64 next_tile = s_tiles[(k + 1) & 3];
+    const wx_i64 tile_base = tile * WX_TILE;
+    const int cur = k & 1;  // t_k is staged in buffer cur, t_{k-2} is read from it first
+    wx_u32 wx_kb = 0;
+    float wx_val[WX_GROUPS][4];
+    wx_u32 lane_pre[WX_GROUPS];
+    // phase 1 (data): evaluate t_k, issue t_{k+1}'s loads, rank t_k
+    if (!control && have) {
+      const wx_u32 wx_rows = (wx_u32)(wx_a.n_rows - tile_base < WX_TILE ? wx_a.n_rows - tile_base : WX_TILE);
+#pragma unroll
+      for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e) {
+          WX_COLS(WX_BIND_TILE_IN)
+          const wx_u32 wx_lrow = (wx_u32)(wx_g * (WX_DTHREADS * 4) + wx_dt * 4 + wx_e);
+          const wx_i64 idx = tile_base + wx_lrow;
+          (void)idx;
+          bool wx_k = wx_lrow < wx_rows;
+          wx_k = wx_k && WX_EVAL_COND();
+          wx_kb |= (wx_k ? 1u : 0u) << (wx_g * 4 + wx_e);
+          wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
+        }
+      }
+      if (next_tile < wx_a.n_tiles) {
+        const wx_i64 wx_tb = next_tile * WX_TILE;
+#pragma unroll
+        for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
+      }
+#pragma unroll
+      for (int g = 0; g < WX_GROUPS; ++g) {
+        wx_u32 pre = 0, tot = 0;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const wx_u64 m = __builtin_amdgcn_ballot_w64(((wx_kb >> (g * 4 + e)) & 1u) != 0u);
+          pre += wx::lanes_below(m);
+          tot += (wx_u32)__builtin_popcountll(m);
+        }
+        lane_pre[g] = pre;
+        if (lane == 0) s_cnt[wave][g] = tot;
+      }
+    }
+    __syncthreads();
+    // phase 2: control publishes t_k's aggregate and fetches the tile of
+    // iteration k + 2; data waves write t_{k-2} out of buffer cur
+    wx_u32 block_total = 0;
+    wx_u32 grp_base[WX_GROUPS];
+    if (have) { WX_BASES(s_cnt) }
+    if (control) {
+      if (lane == 0) {
+        if (have) wx::st_agent(&wx_a.status[tile], (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
+        s_tiles[(k + 2) & 3] = next_tile < wx_a.n_tiles
+                                   ? (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_AGENT)
+                                   : wx_a.n_tiles;
+      }
+    } else if (have2) {
+      const wx_i64 excl = s_excl[cur];  // t_{k-2}'s offset (resolved in iteration k - 1)
+      const wx_i64 prev_base = wx_a.row_base + tile2 * WX_TILE;
+      const float *sv = s_val[cur];
+      const unsigned short *so = s_off[cur];
+      const wx_i64 end = excl + (wx_i64)tot2;
+      wx_i64 b0 = (excl + 31) & ~(wx_i64)31;
+      if (b0 > end) b0 = end;
+      const wx_i64 b1 = b0 + ((end - b0) & ~(wx_i64)3);
+      const int n_head = (int)(b0 - excl), n_edge = n_head + (int)(end - b1);
+      for (int j = wx_dt; j < n_edge; j += WX_DTHREADS) {
+        const wx_i64 pos = j < n_head ? excl + j : b1 + (j - n_head);
+        const int i = (int)(pos - excl);
+        if (wx_a.out_val) wx_a.out_val[pos] = sv[i];
+        if (wx_a.out_idx) {
+          const wx_i64 gi = prev_base + so[i];
+          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
+          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
+        }
+      }
+      for (wx_i64 q = b0 + 4 * (wx_i64)wx_dt; q < b1; q += 4 * (wx_i64)WX_DTHREADS) {
+        const int i = (int)(q - excl);
+        const float v0 = sv[i], v1 = sv[i + 1], v2 = sv[i + 2], v3 = sv[i + 3];
+        const wx_u32 o0 = so[i], o1 = so[i + 1], o2 = so[i + 2], o3 = so[i + 3];
+        if (wx_a.out_val) {
+          typedef float v4f __attribute__((ext_vector_type(4)));
+          const v4f v = {v0, v1, v2, v3};
+          wx::stv(reinterpret_cast<v4f *>(wx_a.out_val + q), v);
+        }
+        if (wx_a.out_idx) {
+          if (wx_a.idx64) {
+            typedef long long v2l __attribute__((ext_vector_type(2)));
+            wx_i64 *o = static_cast<wx_i64 *>(wx_a.out_idx) + q;
+            const v2l x = {(long long)(prev_base + o0), (long long)(prev_base + o1)};
+            const v2l y = {(long long)(prev_base + o2), (long long)(prev_base + o3)};
+            wx::stv(reinterpret_cast<v2l *>(o), x);
+            wx::stv(reinterpret_cast<v2l *>(o + 2), y);
+          } else {
+            typedef int v4i __attribute__((ext_vector_type(4)));
+            const unsigned base = (unsigned)prev_base;
+            const v4i x = {(int)(base + o0), (int)(base + o1), (int)(base + o2), (int)(base + o3)};
+            wx::stv(reinterpret_cast<v4i *>(static_cast<int *>(wx_a.out_idx) + q), x);
+          }
+        }
+      }
+    }
+    __syncthreads();
+    // phase 3: data waves stage t_k into buffer cur; the control wave
+    // resolves t_{k-1}'s offset (published one iteration ago)
+    if (control) {
+      if (have1) {
+        wx_i64 excl = 0;
+        if (tile1 > 0) {
+          excl = wx_lookback(wx_a, tile1);
+          if (lane == 0) wx::st_agent(&wx_a.status[tile1], WX_FLAG_P | (wx_u64)(excl + tot1));
+        }
+        if (lane == 0) {
+          s_excl[cur ^ 1] = excl;  // read when t_{k-1} is written, in iteration k + 1
+          if (tile1 == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + tot1;
+        }
+      }
+    } else if (have) {
+#pragma unroll
+      for (int g = 0; g < WX_GROUPS; ++g) {
+        wx_u32 pos = grp_base[g] + lane_pre[g];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if ((wx_kb >> (g * 4 + e)) & 1u) {
+            s_val[cur][pos] = wx_val[g][e];
+            s_off[cur][pos] = (unsigned short)(g * (WX_DTHREADS * 4) + wx_dt * 4 + e);
+            ++pos;
+          }
+        }
+      }
+    }
+    tile2 = tile1;
+    tot2 = tot1;
+    tile1 = tile;
+    tot1 = have ? block_total : 0u;
+    tile = next_tile;
+  }
+}
+#endif
 
 // One tile per workgroup, taken from a ticket counter (robust fallback).
 extern "C" __global__ __launch_bounds__(WX_DTHREADS) void wx_project_compact_ticket(WxCompactArgs wx_a) {
