@@ -40,6 +40,9 @@ WORKLOADS = {
     "sum": ("SELECT SUM(price * 0.9) FROM t WHERE price > 20", "wx_reduce_sum"),
     "group": ("SELECT SUM(price) FROM t GROUP BY quantity", "wx_group_sum"),
     "topk": ("SELECT discount(price, 0.9) FROM t ORDER BY price DESC LIMIT 5", "wx_topk_scan"),
+    # WarpDB::query's own contract (src/warpdb.cpp:243-256): dense float[N],
+    # 0.0f where WHERE fails, written in the same pass
+    "dense": ("price * quantity WHERE price > 15", "wx_project_dense"),
 }
 
 
@@ -160,6 +163,12 @@ def main():
                               out_v.data_ptr(), out_i.data_ptr(), 4, 0, d_count=counts.data_ptr())
             if world > 1:  # global placement of each shard's rows
                 all_gather(gathered, counts)
+    elif args.workload == "dense":
+        out_v = torch.empty(n, dtype=torch.float32, device="cuda")
+
+        def step(Lx):
+            wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", Lx, wx.MODE_DENSE_FILL,
+                              out_v.data_ptr(), 0, 4, 0)
     elif args.workload == "sum":
         res = torch.zeros(2, dtype=torch.float64, device="cuda")
 
@@ -223,6 +232,8 @@ def main():
         bytes_per_launch = n * 8 + passing * 8
     elif args.workload in ("sum", "topk"):
         bytes_per_launch = n * 4
+    elif args.workload == "dense":
+        bytes_per_launch = n * 12
     else:
         bytes_per_launch = n * 8
     achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
@@ -240,7 +251,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        q = "price * quantity WHERE price > 15" if args.workload == "project" else {
+        q = "price * quantity WHERE price > 15" if args.workload in ("project", "dense") else {
             "sum": "price * 0.9 WHERE price > 20", "group": "price", "topk": "price"}[args.workload]
         cpu = cpu_baseline(q, int(args.cpu_sample))
 

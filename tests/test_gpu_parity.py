@@ -106,6 +106,26 @@ def test_dense_mode_leaves_unselected_rows():
     assert (bits(out.cpu().numpy()) == bits(ref)).all()
 
 
+@pytest.mark.parametrize("n", [1, 4095, 4097, 4 * 256 * 4 * 7 + 5, 1_000_003])
+@pytest.mark.parametrize("offset", [0, 1])
+def test_dense_vs_oracle(n, offset):
+    # src/jit.cpp:55-61: out[idx] = expr where cond; unselected rows untouched
+    # (MODE_DENSE) or 0.0f (MODE_DENSE_FILL, WarpDB::query's zeroed result)
+    cols = synth.c2_table(n)
+    table, _ = dev_table(cols, offset)
+    ht = ora.HostTable(cols)
+    sentinel = np.full(n, -7.0, np.float32)
+    for mode, fill in ((wx.MODE_DENSE, sentinel), (wx.MODE_DENSE_FILL, np.zeros(n, np.float32))):
+        buf = torch.full((n + offset,), -7.0, dtype=torch.float32, device="cuda")
+        out = buf[offset:]
+        wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", launch(), mode,
+                          out.data_ptr())
+        ref = ora.dense(ht, "price * quantity", "price > 15", fill)
+        assert (bits(out.cpu().numpy()) == bits(ref)).all()
+        if offset:
+            assert buf[0].item() == -7.0
+
+
 def test_jit_arch_identity_raw_expression():
     # tests/jit_arch_test.cpp:6-38: the un-lowered expression "price" -> 2.0
     table, _ = dev_table({"price": np.array([2.0], np.float32), "quantity": np.array([0], np.int32)})

@@ -57,6 +57,10 @@ VARIANTS = {
                    "WARPDB_EXTRA_DEFINES": "WX_COMPACT_MINBLOCKS=2"},
     "dw15": {"WARPDB_COMPACT_SCHED": "static"},
     "deep": {},
+    "deep_ntst": {"WARPDB_EXTRA_DEFINES": "WX_NT_STORE=1"},
+    "deep_plainst": {"WARPDB_EXTRA_DEFINES": "WX_DEEP_NT_STORE=0"},
+    "deep_nolookback": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK"},
+    "deep_nostore": {"WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_STORE"},
     "static_sched": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_COMPACT_TICKETS=0"},
     "nolb_unaligned": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK=2"},
     "deep_dw12": {"WARPDB_COMPACT_SCHED": "deep", "WARPDB_COMPACT_DWAVES": "12"},

@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""A/B grid size and unroll of the grid-stride kernels (SUM, GROUP BY, top-K)."""
+"""A/B grid size and unroll of the grid-stride kernels (SUM, GROUP BY, top-K, dense projection)."""
 import os
 import sys
 
@@ -30,10 +30,13 @@ tk = torch.empty(5, device="cuda")
 ti = torch.empty(5, dtype=torch.int64, device="cuda")
 tv = torch.empty(5, device="cuda")
 cnt = torch.zeros(1, dtype=torch.int64, device="cuda")
+dense = torch.empty(n, dtype=torch.float32, device="cuda")
 
 OPS = {
     "sum": (4, lambda Lx: wx.reduce_sum(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", Lx, d_out=res.data_ptr(), want_host=False)),
     "group": (8, lambda Lx: wx.group_sum(table, "price[idx]", "quantity[idx]", None, Lx, 0, cap, gk.data_ptr(), gs.data_ptr(), gc.data_ptr(), d_n_groups=ng.data_ptr(), want_count=False)),
+    "dense": (12, lambda Lx: wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", Lx, wx.MODE_DENSE_FILL, dense.data_ptr())),
+    "dense_masked": (10.5, lambda Lx: wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", Lx, wx.MODE_DENSE, dense.data_ptr())),
     "topk": (4, lambda Lx: wx.topk(table, "price[idx]", None, "discount(price[idx], 0.9f)", 5, True, Lx, tk.data_ptr(), ti.data_ptr(), tv.data_ptr(), d_count=cnt.data_ptr(), want_count=False)),
 }
 EXTRA = os.environ.get("ABL_EXTRA", "")

@@ -11,7 +11,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-K = {"project": "wx_project_compact", "sum": "wx_reduce_sum", "group": "wx_group_sum", "topk": "wx_topk_scan"}
+K = {"project": "wx_project_compact", "sum": "wx_reduce_sum", "group": "wx_group_sum", "topk": "wx_topk_scan", "dense": "wx_project_dense"}
 rnd = sys.argv[1]
 wls = sys.argv[2:] or list(K)
 out = os.path.join(ROOT, "profiles", rnd)

@@ -67,6 +67,13 @@ __device__ __forceinline__ void stv(V *p, V v) {
   *p = v;
 #endif
 }
+template <bool NT, typename V>
+__device__ __forceinline__ void st_sel(V *p, V v) {
+  if constexpr (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
 
 // Four consecutive rows [r0, r0+4) of one column into registers.  Full,
 // aligned groups use 16-byte loads (global_load_dwordx4); the ragged tail
@@ -230,36 +237,74 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 // ===========================================================================
 #if WX_OP == WX_OP_DENSE
 // Dense projection (the reference contract, src/jit.cpp:55-61):
-// out[row] = expr where cond holds.  fill = 1 also writes 0.0f elsewhere.
+// out[row] = expr where cond holds.  fill = 1 also writes 0.0f elsewhere
+// (WarpDB::query's zeroed result in one pass instead of memset + kernel).
+// Same contiguous-span loop as the grid-stride reductions: a workgroup owns
+// WX_BLOCK * WX_UNROLL row quads per iteration and issues all their loads
+// first; each quad's four results leave as one 16-byte store when the quad
+// is full (fill, or every row passing) and as guarded dword stores otherwise.
+// 8 quads per thread, 2 workgroups per CU, nontemporal stores: 2.20 ms per
+// 1e9 rows with fill (12 B/row, 5.45 TB/s), against 2.20-2.34 ms for plain
+// stores across grids and unrolls (profiles/r01/ablate_dense.txt).  Without
+// fill every partially selected 64-B line is a masked write: 3.1 ms.
+#ifndef WX_UNROLL
+#define WX_UNROLL 8
+#endif
+#ifndef WX_DENSE_NT_STORE
+#define WX_DENSE_NT_STORE 1
+#endif
 extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseArgs wx_a) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
   const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
-  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_BLOCK;
-  for (wx_i64 wx_q = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; wx_q < wx_nq; wx_q += wx_stride) {
-    const wx_i64 wx_r0 = wx_q << 2;
-    WX_COLS(WX_DECL_LOAD)
-    float wx_o[4];
-    bool wx_k[4];
+  const wx_i64 wx_nfull = wx_a.n_rows >> 2;
+  for (wx_i64 wx_base = (wx_i64)blockIdx.x * WX_SPAN; wx_base < wx_nq; wx_base += (wx_i64)gridDim.x * WX_SPAN) {
+    WX_COLS(WX_DECL_U)
+    const bool wx_full = WX_ALIGNED16 && wx_base + WX_SPAN <= wx_nfull;
+    if (wx_full) {
 #pragma unroll
-    for (int wx_e = 0; wx_e < 4; ++wx_e) {
-      WX_COLS(WX_BIND_REG)
-      const wx_i64 idx = wx_r0 + wx_e;
-      (void)idx;
-      wx_k[wx_e] = WX_EVAL_COND();
-      wx_o[wx_e] = static_cast<float>(WX_EXPR);
-    }
-    if (wx_a.fill && WX_ALIGNED16 && wx_r0 + 4 <= wx_a.n_rows) {
-      typedef float f4 __attribute__((ext_vector_type(4)));
-      f4 v;
-      v.x = wx_k[0] ? wx_o[0] : 0.0f;
-      v.y = wx_k[1] ? wx_o[1] : 0.0f;
-      v.z = wx_k[2] ? wx_o[2] : 0.0f;
-      v.w = wx_k[3] ? wx_o[3] : 0.0f;
-      *reinterpret_cast<f4 *>(wx_a.out + wx_r0) = v;
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+        const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;
+        WX_COLS(WX_LOAD_U_FAST)
+      }
     } else {
 #pragma unroll
-      for (int wx_e = 0; wx_e < 4; ++wx_e)
-        if (wx_r0 + wx_e < wx_a.n_rows && (wx_k[wx_e] || wx_a.fill))
-          wx_a.out[wx_r0 + wx_e] = wx_k[wx_e] ? wx_o[wx_e] : 0.0f;
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+        const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;
+        WX_COLS(WX_LOAD_U)
+      }
+    }
+#pragma unroll
+    for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+      const wx_i64 wx_r0 = WX_QUAD(wx_u) << 2;
+      if (WX_QUAD(wx_u) >= wx_nq) continue;
+      float wx_o[4];
+      bool wx_k[4];
+#pragma unroll
+      for (int wx_e = 0; wx_e < 4; ++wx_e) {
+        WX_COLS(WX_BIND_U)
+        const wx_i64 idx = wx_r0 + wx_e;
+        (void)idx;
+        wx_k[wx_e] = WX_EVAL_COND();
+        wx_o[wx_e] = static_cast<float>(WX_EXPR);
+      }
+      const bool wx_all = wx_k[0] && wx_k[1] && wx_k[2] && wx_k[3];
+      if (wx_full && (wx_a.fill || wx_all)) {
+        f4 v;
+        v.x = wx_k[0] ? wx_o[0] : 0.0f;
+        v.y = wx_k[1] ? wx_o[1] : 0.0f;
+        v.z = wx_k[2] ? wx_o[2] : 0.0f;
+        v.w = wx_k[3] ? wx_o[3] : 0.0f;
+#if WX_DENSE_NT_STORE
+        __builtin_nontemporal_store(v, reinterpret_cast<f4 *>(wx_a.out + wx_r0));
+#else
+        *reinterpret_cast<f4 *>(wx_a.out + wx_r0) = v;
+#endif
+      } else {
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e)
+          if (wx_r0 + wx_e < wx_a.n_rows && (wx_k[wx_e] || wx_a.fill))
+            wx_a.out[wx_r0 + wx_e] = wx_k[wx_e] ? wx_o[wx_e] : 0.0f;
+      }
     }
   }
 }
@@ -657,7 +702,13 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 // iteration j + 1 (its predecessors' aggregates have long landed), and its
 // output written in iteration j + 2 — the look-back gets a whole iteration
 // of slack instead of half of one.  Two stage buffers (2 x 6 B per tile row),
-// so only compiled when selected.
+// so only compiled when selected.  Its output runs leave with nontemporal
+// stores: 2.23 vs 2.29 ms per 1e9 rows in one process
+// (profiles/r01/ablate_compact_deep_nt.txt; the single-buffer kernel was
+// slower with them, ablate_compact_nt.txt).
+#ifndef WX_DEEP_NT_STORE
+#define WX_DEEP_NT_STORE 1
+#endif
 #if defined(WX_COMPACT_STATIC) && WX_COMPACT_STATIC == 3
 extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx_project_compact_deep(WxCompactArgs wx_a) {
   __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
@@ -769,7 +820,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
         if (wx_a.out_val) {
           typedef float v4f __attribute__((ext_vector_type(4)));
           const v4f v = {v0, v1, v2, v3};
-          wx::stv(reinterpret_cast<v4f *>(wx_a.out_val + q), v);
+          wx::st_sel<WX_DEEP_NT_STORE>(reinterpret_cast<v4f *>(wx_a.out_val + q), v);
         }
         if (wx_a.out_idx) {
           if (wx_a.idx64) {
@@ -777,13 +828,13 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
             wx_i64 *o = static_cast<wx_i64 *>(wx_a.out_idx) + q;
             const v2l x = {(long long)(prev_base + o0), (long long)(prev_base + o1)};
             const v2l y = {(long long)(prev_base + o2), (long long)(prev_base + o3)};
-            wx::stv(reinterpret_cast<v2l *>(o), x);
-            wx::stv(reinterpret_cast<v2l *>(o + 2), y);
+            wx::st_sel<WX_DEEP_NT_STORE>(reinterpret_cast<v2l *>(o), x);
+            wx::st_sel<WX_DEEP_NT_STORE>(reinterpret_cast<v2l *>(o + 2), y);
           } else {
             typedef int v4i __attribute__((ext_vector_type(4)));
             const unsigned base = (unsigned)prev_base;
             const v4i x = {(int)(base + o0), (int)(base + o1), (int)(base + o2), (int)(base + o3)};
-            wx::stv(reinterpret_cast<v4i *>(static_cast<int *>(wx_a.out_idx) + q), x);
+            wx::st_sel<WX_DEEP_NT_STORE>(reinterpret_cast<v4i *>(static_cast<int *>(wx_a.out_idx) + q), x);
           }
         }
       }
