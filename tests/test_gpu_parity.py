@@ -497,3 +497,66 @@ def test_sort_float_and_pairs(n):
         order = np.argsort(keys if asc else -keys.astype(np.int64), kind="stable")
         assert np.array_equal(tk.cpu().numpy(), keys[order])
         assert np.array_equal(tv.cpu().numpy(), v[order])
+
+
+def _sort_input(n, seed):
+    # heavy ties, NaN, -0.0 / +0.0, infinities: the order key must keep equal
+    # keys in input order (stable) and NaN last in both directions
+    u = synth.uniform_f32(n, seed, 0.0, 1.0)
+    v = np.floor(synth.uniform_f32(n, seed + 1, -1000.0, 1000.0)).astype(np.float32) / np.float32(8.0)
+    v[u < 0.01] = np.nan
+    v[(u >= 0.01) & (u < 0.05)] = np.float32(-0.0)
+    v[(u >= 0.05) & (u < 0.09)] = np.float32(0.0)
+    v[(u >= 0.09) & (u < 0.095)] = np.float32(np.inf)
+    v[(u >= 0.095) & (u < 0.1)] = np.float32(-np.inf)
+    return v
+
+
+@pytest.mark.parametrize("n", [8191, 8192, 8193, 3_000_017])
+@pytest.mark.parametrize("sort", ["radix", "bitonic"])
+def test_sort_float_stable_nan_signed_zero(n, sort, monkeypatch):
+    if sort == "bitonic" and n > 10_000:
+        pytest.skip("bitonic cross-check at small sizes only")
+    monkeypatch.setenv("WARPDB_SORT", sort)
+    v = _sort_input(n, 11)
+    for asc in (True, False):
+        t = torch.from_numpy(v.copy()).cuda()
+        wx.sort_float(t.data_ptr(), n, asc, launch())
+        ref = v[np.argsort(v if asc else -v, kind="stable")]
+        assert np.array_equal(bits(t.cpu().numpy()), bits(ref))
+
+
+@pytest.mark.parametrize("n", [100_003, 2_500_001])
+@pytest.mark.parametrize("span", ["narrow", "full"])
+def test_sort_pairs_radix_stable(n, span):
+    # narrow keys leave three digits constant (those passes are skipped);
+    # full-range keys include INT_MIN / INT_MAX.  Payload = input position,
+    # so the payload order proves stability.
+    if span == "narrow":
+        keys = synth.uniform_int(n, 5, 0, 99).astype(np.int32)
+    else:
+        keys = (synth.uniform_int(n, 6, 0, (1 << 32) - 1).astype(np.int64) - (1 << 31)).astype(np.int32)
+        keys[:3] = [np.iinfo(np.int32).min, np.iinfo(np.int32).max, 0]
+        keys[n // 2:n // 2 + 1000] = 7  # a long run of ties
+    pos = np.arange(n, dtype=np.float32)
+    for asc in (True, False):
+        tk = torch.from_numpy(keys.copy()).cuda()
+        tv = torch.from_numpy(pos.copy()).cuda()
+        wx.sort_pairs(tk.data_ptr(), tv.data_ptr(), n, asc, launch())
+        order = np.argsort(keys if asc else -keys.astype(np.int64), kind="stable")
+        assert np.array_equal(tk.cpu().numpy(), keys[order])
+        assert np.array_equal(tv.cpu().numpy(), pos[order])
+
+
+def test_sort_radix_large_properties():
+    # 2^27 + 5 keys (16 385 tiles per pass): sortedness, and the multiset is
+    # unchanged (sum of bit patterns and of squares of bit patterns as int64)
+    n = (1 << 27) + 5
+    t = torch.empty(n, dtype=torch.float32, device="cuda")
+    wx.fill_synthetic(t.data_ptr(), wx.FLOAT32, n, 21, 0, -50.0, 50.0, launch())
+    b0 = t.view(torch.int32).to(torch.int64)
+    s0, q0 = b0.sum().item(), (b0 * b0).sum().item()
+    wx.sort_float(t.data_ptr(), n, True, launch())
+    assert bool((t[1:] >= t[:-1]).all().item())
+    b1 = t.view(torch.int32).to(torch.int64)
+    assert (b1.sum().item(), (b1 * b1).sum().item()) == (s0, q0)

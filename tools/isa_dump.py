@@ -1,6 +1,6 @@
 """Dump the gfx950 assembly + resource usage of one generated kernel family.
 
-usage: python tools/isa_dump.py {compact,sum,group,topk} [EXTRA_DEFINES]
+usage: python tools/isa_dump.py {compact,sum,group,topk,util} [EXTRA_DEFINES]
 Writes /tmp/wx_<op>.hip and /tmp/wx_<op>.s and prints vgpr/sgpr/scratch/LDS
 per kernel (offline hipcc compile of the exact source the runtime builds).
 """
@@ -23,6 +23,7 @@ jobs = {
     "sum": (t, wx.OP_SUM, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", None, 0),
     "group": (t_int, wx.OP_GROUP, "price[idx]", None, "quantity[idx]", 0),
     "topk": (t, wx.OP_TOPK, "price[idx]", None, "(price[idx] * 0.9f)", 5),
+    "util": (None, wx.OP_UTIL, None, None, None, 0),
 }
 table, o, e, c, aux, k = jobs[op]
 src = wx.prepare(table, o, e, c, aux, k, want_source=True)

@@ -37,6 +37,17 @@ typedef unsigned int wx_u32;
 #define WX_TOPK_SLOTS 64        // top-K grid-wide bound: one slot per wave lane
 #define WX_TOPK_SLOT_STRIDE 64  // u32 elements between slots (256 B)
 #define WX_SORT_LDS (WX_BLOCK * 8)
+// LSD radix sort (wx_radix_*): 8-bit digits, 4 passes over 32-bit keys;
+// one tile = WX_RS_BLOCK threads x WX_RS_ITEMS keys, one 64-bit look-back
+// status word per (tile, digit).
+#ifndef WX_RS_BLOCK
+#define WX_RS_BLOCK 512  // >= 256: threads 0..255 own one digit each
+#endif
+#ifndef WX_RS_ITEMS
+#define WX_RS_ITEMS 16
+#endif
+#define WX_RS_TILE (WX_RS_BLOCK * WX_RS_ITEMS)
+#define WX_RS_EPOCHS 63
 
 struct WxDenseArgs {
   const void *col[WX_MAX_COLS];
@@ -172,6 +183,30 @@ struct WxSortApplyArgs {
   void *dst_a;
   const float *src_v;
   float *dst_v;
+};
+
+struct WxRadixHistArgs {
+  const wx_u32 *src;
+  wx_i64 n;
+  wx_u32 *hist;  // [4][256], zeroed by the host
+  int kind;      // 0 float values, 1 int keys
+  int ascending;
+};
+
+struct WxRadixPassArgs {
+  const wx_u32 *src_k;
+  wx_u32 *dst_k;
+  const wx_u32 *src_v;  // payload (pairs) or null
+  wx_u32 *dst_v;
+  const wx_u32 *digit_base;  // [256]: first output slot of each digit
+  wx_u64 *status;            // [n_tiles][256] look-back words {epoch:6 | flag:2 | count:56}
+  wx_u32 *ctl;               // [0] tile ticket, [1] abort word
+  wx_u32 *err;               // sticky device error bits (workspace ctrs[1])
+  wx_i64 n;
+  int shift;
+  int kind;
+  int ascending;
+  wx_u32 epoch;  // 1..WX_RS_EPOCHS
 };
 
 struct WxSumFinArgs {

@@ -1747,4 +1747,252 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApply
     if (a.src_v) a.dst_v[r] = a.src_v[p];
   }
 }
+
+// ---------------------------------------------------------------------------
+// LSD radix sort for the jit_sort_* entry points (src/jit.cpp:248-307): four
+// stable passes of 8-bit digits over a 32-bit order key computed on the fly
+// from the element itself (floats: the order map with -0.0 == +0.0 and NaN
+// last; ints: sign flip; descending: the complement), so float sorts move
+// only their 4-byte values and pair sorts their key + payload.
+//
+// wx_radix_hist: one read of the input builds the histograms of all four
+// digits (per-workgroup LDS counters; a wave whose lanes share a digit adds
+// once).  The host scans them into per-digit output bases and skips a pass
+// whose digit is the same for every key.
+//
+// wx_radix_pass (one pass, "onesweep"): a workgroup takes tile t from a
+// ticket counter, loads WX_RS_ITEMS keys per lane wave-striped (key i of
+// lane l of wave w at t*TILE + w*64*ITEMS + i*64 + l, so rank order is input
+// order), and ranks each key inside its wave by matching digits with eight
+// ballots: the lowest lane of every digit group bumps the wave's LDS counter
+// and broadcasts the old count.  Threads 0..255 then own one digit each:
+// prefix over the waves, publish the tile's count {A}, look back over the
+// preceding tiles' words of the same digit until an inclusive {P} word, and
+// publish {P}.  Keys are permuted into digit order in LDS and written out
+// from there, so consecutive lanes write consecutive addresses of a digit's
+// run.  Every wait is bounded: a timed-out waiter raises WX_DEVERR_LOOKBACK
+// and the abort word, and the launch drains.
+#define WX_RS_WAVES (WX_RS_BLOCK / 64)
+#ifndef WX_RS_LBW
+#define WX_RS_LBW 8  // predecessor words per digit per look-back round
+#endif
+#ifndef WX_SPIN_LIMIT
+#define WX_SPIN_LIMIT (1u << 20)
+#endif
+#define WX_RS_FLAG_A (1ull << 56)
+#define WX_RS_FLAG_P (2ull << 56)
+#define WX_RS_VAL_MASK ((1ull << 56) - 1ull)
+
+__device__ __forceinline__ wx_u32 wx_rs_key(wx_u32 x, int kind, int asc) {
+  wx_u32 r;
+  if (kind == 0) {
+    r = wx::f2ord(__uint_as_float(x));
+    if (r == 0u) return 0xffffffffu;  // NaN last in either direction
+  } else {
+    r = x ^ 0x80000000u;
+  }
+  return asc ? r : ~r;
+}
+
+#ifndef WX_RS_HCOPIES
+#define WX_RS_HCOPIES 8  // LDS histogram copies, picked by lane % copies: few-valued digits conflict 8x less
+#endif
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist(WxRadixHistArgs a) {
+  __shared__ wx_u32 h[4 * 256 * WX_RS_HCOPIES];  // [digit][bin][copy]
+  for (int i = threadIdx.x; i < 4 * 256 * WX_RS_HCOPIES; i += WX_BLOCK) h[i] = 0u;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int copy = lane % WX_RS_HCOPIES;
+  const wx_i64 span = (wx_i64)WX_BLOCK * 8;
+  for (wx_i64 base = (wx_i64)blockIdx.x * span; base < a.n; base += (wx_i64)gridDim.x * span) {
+    wx_u32 x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const wx_i64 i = base + (wx_i64)u * WX_BLOCK + threadIdx.x;
+      x[u] = i < a.n ? wx::ldv(a.src + i) : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const wx_i64 i = base + (wx_i64)u * WX_BLOCK + threadIdx.x;
+      if (i < a.n) {
+        const wx_u32 k = wx_rs_key(x[u], a.kind, a.ascending);
+        const wx_u64 act = __builtin_amdgcn_ballot_w64(true);
+        const int first = __builtin_ctzll(act);
+#pragma unroll
+        for (int p = 0; p < 4; ++p) {
+          const wx_u32 d = (k >> (8 * p)) & 255u;
+          const wx_u32 d0 = __builtin_amdgcn_readfirstlane(d);
+          if (__builtin_amdgcn_ballot_w64(d != d0) == 0ull) {
+            if (lane == first) atomicAdd(&h[(p * 256 + d0) * WX_RS_HCOPIES], (wx_u32)__builtin_popcountll(act));
+          } else {
+            atomicAdd(&h[(p * 256 + d) * WX_RS_HCOPIES + copy], 1u);
+          }
+        }
+      }
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 4 * 256; i += WX_BLOCK) {
+    wx_u32 c = 0u;
+#pragma unroll
+    for (int j = 0; j < WX_RS_HCOPIES; ++j) c += h[i * WX_RS_HCOPIES + j];
+    if (c) atomicAdd(&a.hist[i], c);
+  }
+}
+
+template <bool PAY>
+__device__ __forceinline__ void wx_radix_pass_impl(const WxRadixPassArgs &a, wx_u32 *s_k, wx_u32 *s_v) {
+  __shared__ wx_u32 s_wc[WX_RS_WAVES][256];  // per-wave digit counts, then their exclusive prefix
+  __shared__ wx_u32 s_gb[256];               // output slot of digit d's first key minus its tile offset
+  __shared__ wx_u32 s_ld[256];               // tile-local exclusive prefix of the digit counts
+  __shared__ wx_u32 s_wsum[4];
+  __shared__ wx_u32 s_tile;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_tile = atomicAdd(&a.ctl[0], 1u);
+  for (int i = tid; i < WX_RS_WAVES * 256; i += WX_RS_BLOCK) (&s_wc[0][0])[i] = 0u;
+  __syncthreads();
+  const wx_u32 tile = s_tile;
+  const wx_i64 tb = (wx_i64)tile * WX_RS_TILE;
+  const wx_i64 wb = tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane;
+  wx_u32 x[WX_RS_ITEMS], v[WX_RS_ITEMS], rk[WX_RS_ITEMS];
+#pragma unroll
+  for (int i = 0; i < WX_RS_ITEMS; ++i) {
+    const wx_i64 e = wb + (wx_i64)i * 64;
+    x[i] = e < a.n ? wx::ldv(a.src_k + e) : 0u;
+    if (PAY) v[i] = e < a.n ? wx::ldv(a.src_v + e) : 0u;
+  }
+  const wx_u64 below = (1ull << lane) - 1ull;
+#pragma unroll
+  for (int i = 0; i < WX_RS_ITEMS; ++i) {
+    const bool valid = wb + (wx_i64)i * 64 < a.n;
+    const wx_u32 d = (wx_rs_key(x[i], a.kind, a.ascending) >> a.shift) & 255u;
+    wx_u64 m = __builtin_amdgcn_ballot_w64(valid);
+#pragma unroll
+    for (int b = 0; b < 8; ++b) {
+      const bool bit = (d >> b) & 1u;
+      const wx_u64 bb = __builtin_amdgcn_ballot_w64(bit);
+      m &= bit ? bb : ~bb;
+    }
+    const int leader = valid ? __builtin_ctzll(m) : lane;
+    wx_u32 old = 0u;
+    if (valid && lane == leader) {
+      old = s_wc[wave][d];
+      s_wc[wave][d] = old + (wx_u32)__builtin_popcountll(m);
+    }
+    old = __shfl(old, leader);
+    rk[i] = old + (wx_u32)__builtin_popcountll(m & below);
+    __builtin_amdgcn_wave_barrier();
+  }
+  __syncthreads();
+  // threads 0..255: digit tid
+  wx_u32 tot = 0u, inc = 0u;
+  if (tid < 256) {
+#pragma unroll
+    for (int w = 0; w < WX_RS_WAVES; ++w) {
+      const wx_u32 c = s_wc[w][tid];
+      s_wc[w][tid] = tot;
+      tot += c;
+    }
+    inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_u32 t = __shfl_up(inc, o);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) s_wsum[wave] = inc;
+  }
+  __syncthreads();
+  if (tid < 256) {
+    wx_u32 ld = inc - tot;
+    for (int w = 0; w < wave; ++w) ld += s_wsum[w];
+    const wx_u64 E = (wx_u64)a.epoch << 58;
+    wx_u64 *row = a.status + (wx_u64)tile * 256;
+    wx_u64 excl = 0;
+#ifndef WX_RS_DIAG_NO_LOOKBACK
+#define WX_RS_DIAG_NO_LOOKBACK 0  // diagnostic: every tile takes its offset as 0 (results invalid)
+#endif
+    if (tile == 0 || WX_RS_DIAG_NO_LOOKBACK) {
+      wx::st_agent(&row[tid], E | WX_RS_FLAG_P | tot);
+    } else {
+      wx::st_agent(&row[tid], E | WX_RS_FLAG_A | tot);
+      // WX_RS_LBW predecessors per round, loads in flight together; stop at
+      // the first unpublished word (re-polled from there) or the first {P}
+      wx_i64 p = (wx_i64)tile - 1;
+      wx_u32 spins = 0;
+      while (true) {
+        wx_u64 wv[WX_RS_LBW];
+#pragma unroll
+        for (int j = 0; j < WX_RS_LBW; ++j)
+          wv[j] = p - j >= 0 ? wx::ld_agent(&a.status[(wx_u64)(p - j) * 256 + tid]) : (E | WX_RS_FLAG_P);
+        int stop = WX_RS_LBW;  // index of the first unpublished word
+        bool done = false;
+#pragma unroll
+        for (int j = 0; j < WX_RS_LBW; ++j) {
+          if (stop == WX_RS_LBW && !done) {
+            const wx_u64 flag = (wv[j] >> 56) & 3ull;
+            if ((wv[j] >> 58) != (wx_u64)a.epoch || flag == 0ull) {
+              stop = j;
+            } else {
+              excl += wv[j] & WX_RS_VAL_MASK;
+              done = flag == 2ull;
+            }
+          }
+        }
+        if (done) break;
+        if (stop == WX_RS_LBW) {
+          p -= WX_RS_LBW;
+          continue;
+        }
+        p -= stop;
+        __builtin_amdgcn_s_sleep(1);
+        if ((++spins & 63u) == 0u) {
+          if (spins > WX_SPIN_LIMIT) {
+            atomicOr(a.err, WX_DEVERR_LOOKBACK);
+            atomicExch(&a.ctl[1], 1u);
+          }
+          if (__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+        }
+      }
+      wx::st_agent(&row[tid], E | WX_RS_FLAG_P | (excl + tot));
+    }
+    s_gb[tid] = a.digit_base[tid] + (wx_u32)excl - ld;
+    s_ld[tid] = ld;
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < WX_RS_ITEMS; ++i) {
+    if (wb + (wx_i64)i * 64 < a.n) {
+      const wx_u32 d = (wx_rs_key(x[i], a.kind, a.ascending) >> a.shift) & 255u;
+      const wx_u32 pos = s_ld[d] + s_wc[wave][d] + rk[i];
+      s_k[pos] = x[i];
+      if (PAY) s_v[pos] = v[i];
+    }
+  }
+  __syncthreads();
+  const wx_i64 rem = a.n - tb;
+  const int tile_n = rem < WX_RS_TILE ? (int)rem : WX_RS_TILE;
+#pragma unroll
+  for (int j = 0; j < WX_RS_ITEMS; ++j) {
+    const int pos = j * WX_RS_BLOCK + tid;
+    if (pos < tile_n) {
+      const wx_u32 xk = s_k[pos];
+      const wx_u32 d = (wx_rs_key(xk, a.kind, a.ascending) >> a.shift) & 255u;
+      wx_u32 g = s_gb[d] + (wx_u32)pos;
+      if (WX_RS_DIAG_NO_LOOKBACK) g = (wx_u32)min((wx_i64)g, a.n - 1);
+      a.dst_k[g] = xk;
+      if (PAY) a.dst_v[g] = s_v[pos];
+    }
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_RS_BLOCK) void wx_radix_pass_k(WxRadixPassArgs a) {
+  __shared__ wx_u32 s_k[WX_RS_TILE];
+  wx_radix_pass_impl<false>(a, s_k, nullptr);
+}
+
+extern "C" __global__ __launch_bounds__(WX_RS_BLOCK) void wx_radix_pass_kv(WxRadixPassArgs a) {
+  __shared__ wx_u32 s_k[WX_RS_TILE];
+  __shared__ wx_u32 s_v[WX_RS_TILE];
+  wx_radix_pass_impl<true>(a, s_k, s_v);
+}
 #endif
