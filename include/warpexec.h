@@ -14,6 +14,7 @@
  *   wx_group_sum        jit_group_sum            include/jit.hpp:15-18, src/jit.cpp:179-246
  *   wx_sort_pairs       jit_sort_pairs           include/jit.hpp:22-23, src/jit.cpp:248-281
  *   wx_sort_float       jit_sort_float           include/jit.hpp:26-27, src/jit.cpp:283-307
+ *   wx_sort_by_key      ORDER BY <expr> keyed sort  src/warpdb.cpp:470-476
  *   wx_topk             jit_sort_float + LIMIT   src/warpdb.cpp:453-455,483-495
  *   wx_reduce_sum       per-shard SUM of query_multi_gpu (new; the reference
  *                       gathers dense results on the host, src/multi_gpu_utils.cpp:5-63)
@@ -161,6 +162,12 @@ wx_status wx_sort_pairs(int32_t *d_keys, float *d_vals, int64_t count, int32_t a
                         const wx_launch *launch, char *err, size_t errlen);
 wx_status wx_sort_float(float *d_vals, int64_t count, int32_t ascending, const wx_launch *launch,
                         char *err, size_t errlen);
+/* Stable sort of float keys carrying a 4-byte payload (the ORDER BY key of
+ * each selected row and its SELECT value: the keyed sort query_sql intends,
+ * src/warpdb.cpp:470-476).  Same order as wx_sort_float: NaN keys last,
+ * -0.0 == +0.0, ties keep their input order. */
+wx_status wx_sort_by_key(float *d_keys, float *d_vals, int64_t count, int32_t ascending,
+                         const wx_launch *launch, char *err, size_t errlen);
 
 /* Seeded synthetic column generator (counter-based, so every shard can
  * generate its own rows on the device):  h = splitmix64(row + seed * 0xD1B54A32D192ED03)

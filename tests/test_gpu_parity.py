@@ -512,7 +512,7 @@ def _sort_input(n, seed):
     return v
 
 
-@pytest.mark.parametrize("n", [8191, 8192, 8193, 3_000_017])
+@pytest.mark.parametrize("n", [8191, 10240, 10241, 24577, 3_000_017])
 @pytest.mark.parametrize("sort", ["radix", "bitonic"])
 def test_sort_float_stable_nan_signed_zero(n, sort, monkeypatch):
     if sort == "bitonic" and n > 10_000:
@@ -526,7 +526,7 @@ def test_sort_float_stable_nan_signed_zero(n, sort, monkeypatch):
         assert np.array_equal(bits(t.cpu().numpy()), bits(ref))
 
 
-@pytest.mark.parametrize("n", [100_003, 2_500_001])
+@pytest.mark.parametrize("n", [12288, 12289, 100_003, 2_500_001])
 @pytest.mark.parametrize("span", ["narrow", "full"])
 def test_sort_pairs_radix_stable(n, span):
     # narrow keys leave three digits constant (those passes are skipped);
@@ -545,6 +545,25 @@ def test_sort_pairs_radix_stable(n, span):
         wx.sort_pairs(tk.data_ptr(), tv.data_ptr(), n, asc, launch())
         order = np.argsort(keys if asc else -keys.astype(np.int64), kind="stable")
         assert np.array_equal(tk.cpu().numpy(), keys[order])
+        assert np.array_equal(tv.cpu().numpy(), pos[order])
+
+
+@pytest.mark.parametrize("n", [1, 12289, 1_000_003])
+@pytest.mark.parametrize("sort", ["radix", "bitonic"])
+def test_sort_by_key_stable(n, sort, monkeypatch):
+    # the keyed sort behind query_sql ORDER BY <other expression>: float keys
+    # with NaN / +-0 / ties, payload = input position (proves stability)
+    if sort == "bitonic" and n > 100_000:
+        pytest.skip("bitonic cross-check at small sizes only")
+    monkeypatch.setenv("WARPDB_SORT", sort)
+    k = _sort_input(n, 23)
+    pos = np.arange(n, dtype=np.float32)
+    for asc in (True, False):
+        tk = torch.from_numpy(k.copy()).cuda()
+        tv = torch.from_numpy(pos.copy()).cuda()
+        wx.sort_by_key(tk.data_ptr(), tv.data_ptr(), n, asc, launch())
+        order = np.argsort(k if asc else -k, kind="stable")
+        assert np.array_equal(bits(tk.cpu().numpy()), bits(k[order]))
         assert np.array_equal(tv.cpu().numpy(), pos[order])
 
 

@@ -102,6 +102,32 @@ def test_query_sql_reference_expectations():
     assert db.query_sql("SELECT price * 2 FROM test WHERE quantity > 3") == [40.0, 60.0]
 
 
+def test_query_sql_order_by_other_expression(tmp_path):
+    # ORDER BY an expression other than the SELECT one, any LIMIT / OFFSET:
+    # keyed device sort (src/warpdb.cpp:470-476), ties by row order, against
+    # the oracle's stable ORDER BY (ora_topk with k = every row)
+    n = 20_011
+    cols = synth.c2_table(n)
+    cols["price"] = (np.floor(cols["price"] * 4) / 4).astype(np.float32)  # ties
+    path = tmp_path / "o.csv"
+    with open(path, "w") as f:
+        f.write("price,quantity\n")
+        for p, q in zip(cols["price"], cols["quantity"]):
+            f.write(f"{float(p)!r},{int(q)}\n")
+    db = pw().WarpDB(str(path))
+    ht = ora.HostTable(cols)
+    for desc in (True, False):
+        d = "DESC" if desc else "ASC"
+        _, _, rv = ora.topk(ht, "price", n, desc, cond="price > 15", select_expr="quantity * 2")
+        got = db.query_sql(f"SELECT quantity * 2 FROM t WHERE price > 15 ORDER BY price {d}")
+        assert np.array_equal(np.array(got, np.float32), rv)
+        got = db.query_sql(f"SELECT quantity * 2 FROM t WHERE price > 15 ORDER BY price {d} OFFSET 7 LIMIT 100")
+        assert np.array_equal(np.array(got, np.float32), rv[7:107])
+    # same expression, LIMIT beyond the top-K kernel's 32: full sort + slice
+    _, _, rv = ora.topk(ht, "price", 100, True)
+    assert np.array_equal(np.array(db.query_sql("SELECT price FROM t ORDER BY price DESC LIMIT 100"), np.float32), rv)
+
+
 def test_query_sql_min_max():
     # AggData min / max (src/warpdb.cpp:375-385, 387-418) on data/test.csv:
     # price [10.5, 20, 15.25, 30], quantity [3, 4, 2, 5]

@@ -48,6 +48,7 @@ EXPORTED_SYMBOLS = (
     "wx_topk",
     "wx_sort_pairs",
     "wx_sort_float",
+    "wx_sort_by_key",
     "wx_fill_synthetic",
     "wx_prepare",
     "wx_check",
@@ -116,6 +117,7 @@ def load() -> ctypes.CDLL:
         "wx_topk": [T, E, E, E, I32, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_sort_pairs": [P, P, I64, I32, L, E, S],
         "wx_sort_float": [P, I64, I32, L, E, S],
+        "wx_sort_by_key": [P, P, I64, I32, L, E, S],
         "wx_fill_synthetic": [P, I32, I64, U64, I32, D, D, I64, L, E, S],
         "wx_prepare": [T, I32, E, E, E, I32, L, E, S, E, S],
         "wx_check": [L, E, S],
@@ -280,6 +282,12 @@ def sort_float(d_vals: int, count: int, ascending: bool, launch: WxLaunch) -> No
     lib = load()
     err = _err()
     _check(lib.wx_sort_float(d_vals, count, 1 if ascending else 0, ctypes.byref(launch), err, len(err)), err)
+
+
+def sort_by_key(d_keys: int, d_vals: int, count: int, ascending: bool, launch: WxLaunch) -> None:
+    lib = load()
+    err = _err()
+    _check(lib.wx_sort_by_key(d_keys, d_vals, count, 1 if ascending else 0, ctypes.byref(launch), err, len(err)), err)
 
 
 def fill_synthetic(d_ptr: int, dtype: int, n: int, seed: int, kind: int, lo: float, hi: float,

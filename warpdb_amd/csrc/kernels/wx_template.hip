@@ -1760,7 +1760,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApply
 // once).  The host scans them into per-digit output bases and skips a pass
 // whose digit is the same for every key.
 //
-// wx_radix_pass (one pass, "onesweep"): a workgroup takes tile t from a
+// wx_radix_sweep_* (one pass, "onesweep"): a workgroup takes tile t from a
 // ticket counter, loads WX_RS_ITEMS keys per lane wave-striped (key i of
 // lane l of wave w at t*TILE + w*64*ITEMS + i*64 + l, so rank order is input
 // order), and ranks each key inside its wave by matching digits with eight
@@ -1774,7 +1774,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApply
 // and the abort word, and the launch drains.
 #define WX_RS_WAVES (WX_RS_BLOCK / 64)
 #ifndef WX_RS_LBW
-#define WX_RS_LBW 8  // predecessor words per digit per look-back round
+#define WX_RS_LBW 1  // predecessor words per digit per look-back round (8 measured slower: poll traffic)
 #endif
 #ifndef WX_SPIN_LIMIT
 #define WX_SPIN_LIMIT (1u << 20)
@@ -1840,32 +1840,79 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist(WxRadixHist
   }
 }
 
-template <bool PAY>
-__device__ __forceinline__ void wx_radix_pass_impl(const WxRadixPassArgs &a, wx_u32 *s_k, wx_u32 *s_v) {
-  __shared__ wx_u32 s_wc[WX_RS_WAVES][256];  // per-wave digit counts, then their exclusive prefix
-  __shared__ wx_u32 s_gb[256];               // output slot of digit d's first key minus its tile offset
-  __shared__ wx_u32 s_ld[256];               // tile-local exclusive prefix of the digit counts
-  __shared__ wx_u32 s_wsum[4];
-  __shared__ wx_u32 s_tile;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_tile = atomicAdd(&a.ctl[0], 1u);
-  for (int i = tid; i < WX_RS_WAVES * 256; i += WX_RS_BLOCK) (&s_wc[0][0])[i] = 0u;
-  __syncthreads();
-  const wx_u32 tile = s_tile;
-  const wx_i64 tb = (wx_i64)tile * WX_RS_TILE;
-  const wx_i64 wb = tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane;
-  wx_u32 x[WX_RS_ITEMS], v[WX_RS_ITEMS], rk[WX_RS_ITEMS];
-#pragma unroll
-  for (int i = 0; i < WX_RS_ITEMS; ++i) {
-    const wx_i64 e = wb + (wx_i64)i * 64;
-    x[i] = e < a.n ? wx::ldv(a.src_k + e) : 0u;
-    if (PAY) v[i] = e < a.n ? wx::ldv(a.src_v + e) : 0u;
+#ifndef WX_RS_DIAG_NO_LOOKBACK
+#define WX_RS_DIAG_NO_LOOKBACK 0  // diagnostic: every tile takes its offset as 0 (results invalid)
+#endif
+#ifndef WX_RS_MATCH_LDS
+// Digit peers of a key by one ds_or_b64 of the lane's bit into a per-digit
+// LDS mask (then read back and cleared): 3 LDS operations per key instead of
+// eight ballots and ~70 VALU instructions.  0 selects the ballot form.
+#define WX_RS_MATCH_LDS 1
+#endif
+
+// Order key with the direction and key kind known at compile time.
+template <int KIND, bool ASC>
+__device__ __forceinline__ wx_u32 wx_rs_key_t(wx_u32 x) {
+  wx_u32 r;
+  if constexpr (KIND == 0) {
+    r = wx::f2ord(__uint_as_float(x));
+    if (r == 0u) return 0xffffffffu;  // NaN last in either direction
+  } else {
+    r = x ^ 0x80000000u;
   }
+  return ASC ? r : ~r;
+}
+
+struct WxRsShared {
+  wx_u32 wc[WX_RS_WAVES][256];  // per-wave digit counts, then their exclusive prefix over the waves
+#if WX_RS_MATCH_LDS
+  wx_u64 peers[WX_RS_WAVES][256];  // per-wave digit peer masks (zero between keys)
+#endif
+  wx_u32 gb[256];  // output slot of digit d's first key minus its tile-local offset
+  wx_u32 ld[256];  // tile-local exclusive prefix of the digit counts
+  wx_u32 wsum[4];
+  wx_u32 tk[2];  // tile ticket
+};
+
+template <bool PAY>
+__device__ __forceinline__ void wx_rs_load(const WxRadixPassArgs &a, wx_i64 wb, bool whole, wx_u32 (&x)[WX_RS_ITEMS],
+                                           wx_u32 (&v)[WX_RS_ITEMS]) {
+  if (whole) {  // tile-uniform: unguarded loads
+#pragma unroll
+    for (int i = 0; i < WX_RS_ITEMS; ++i) {
+      x[i] = wx::ldv(a.src_k + wb + (wx_i64)i * 64);
+      if (PAY) v[i] = wx::ldv(a.src_v + wb + (wx_i64)i * 64);
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < WX_RS_ITEMS; ++i) {
+      const wx_i64 e = wb + (wx_i64)i * 64;
+      x[i] = e < a.n ? wx::ldv(a.src_k + e) : 0u;
+      if (PAY) v[i] = e < a.n ? wx::ldv(a.src_v + e) : 0u;
+    }
+  }
+}
+
+// In-wave stable rank of each key among the wave's keys with the same digit:
+// the group's lowest lane bumps the wave's count and broadcasts the old one.
+template <int KIND, bool ASC>
+__device__ __forceinline__ void wx_rs_rank(const WxRadixPassArgs &a, WxRsShared &S, wx_i64 wb,
+                                           const wx_u32 (&x)[WX_RS_ITEMS], wx_u32 (&rk)[WX_RS_ITEMS]) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const wx_u64 below = (1ull << lane) - 1ull;
 #pragma unroll
   for (int i = 0; i < WX_RS_ITEMS; ++i) {
     const bool valid = wb + (wx_i64)i * 64 < a.n;
-    const wx_u32 d = (wx_rs_key(x[i], a.kind, a.ascending) >> a.shift) & 255u;
+    const wx_u32 d = (wx_rs_key_t<KIND, ASC>(x[i]) >> a.shift) & 255u;
+#if WX_RS_MATCH_LDS
+    wx_u64 m = 0ull;
+    if (valid) {
+      atomicOr(&S.peers[wave][d], 1ull << lane);
+      m = __hip_atomic_load(&S.peers[wave][d], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+    }
+    __builtin_amdgcn_wave_barrier();
+    if (valid) __hip_atomic_store(&S.peers[wave][d], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#else
     wx_u64 m = __builtin_amdgcn_ballot_w64(valid);
 #pragma unroll
     for (int b = 0; b < 8; ++b) {
@@ -1873,24 +1920,27 @@ __device__ __forceinline__ void wx_radix_pass_impl(const WxRadixPassArgs &a, wx_
       const wx_u64 bb = __builtin_amdgcn_ballot_w64(bit);
       m &= bit ? bb : ~bb;
     }
+#endif
     const int leader = valid ? __builtin_ctzll(m) : lane;
     wx_u32 old = 0u;
-    if (valid && lane == leader) {
-      old = s_wc[wave][d];
-      s_wc[wave][d] = old + (wx_u32)__builtin_popcountll(m);
-    }
+    if (valid && lane == leader) old = atomicAdd(&S.wc[wave][d], (wx_u32)__builtin_popcountll(m));
     old = __shfl(old, leader);
     rk[i] = old + (wx_u32)__builtin_popcountll(m & below);
     __builtin_amdgcn_wave_barrier();
   }
-  __syncthreads();
-  // threads 0..255: digit tid
+}
+
+// Threads 0..255, digit d = tid: exclusive prefix over the waves and over the
+// digits, publish {A}, look back to an inclusive {P}, publish {P}; fills
+// S.gb / S.ld.  Called by every thread (it holds a barrier).
+__device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   wx_u32 tot = 0u, inc = 0u;
   if (tid < 256) {
 #pragma unroll
     for (int w = 0; w < WX_RS_WAVES; ++w) {
-      const wx_u32 c = s_wc[w][tid];
-      s_wc[w][tid] = tot;
+      const wx_u32 c = S.wc[w][tid];
+      S.wc[w][tid] = tot;
       tot += c;
     }
     inc = tot;
@@ -1899,18 +1949,15 @@ __device__ __forceinline__ void wx_radix_pass_impl(const WxRadixPassArgs &a, wx_
       const wx_u32 t = __shfl_up(inc, o);
       if (lane >= o) inc += t;
     }
-    if (lane == 63) s_wsum[wave] = inc;
+    if (lane == 63) S.wsum[wave] = inc;
   }
   __syncthreads();
   if (tid < 256) {
     wx_u32 ld = inc - tot;
-    for (int w = 0; w < wave; ++w) ld += s_wsum[w];
+    for (int w = 0; w < wave; ++w) ld += S.wsum[w];
     const wx_u64 E = (wx_u64)a.epoch << 58;
     wx_u64 *row = a.status + (wx_u64)tile * 256;
     wx_u64 excl = 0;
-#ifndef WX_RS_DIAG_NO_LOOKBACK
-#define WX_RS_DIAG_NO_LOOKBACK 0  // diagnostic: every tile takes its offset as 0 (results invalid)
-#endif
     if (tile == 0 || WX_RS_DIAG_NO_LOOKBACK) {
       wx::st_agent(&row[tid], E | WX_RS_FLAG_P | tot);
     } else {
@@ -1955,44 +2002,110 @@ __device__ __forceinline__ void wx_radix_pass_impl(const WxRadixPassArgs &a, wx_
       }
       wx::st_agent(&row[tid], E | WX_RS_FLAG_P | (excl + tot));
     }
-    s_gb[tid] = a.digit_base[tid] + (wx_u32)excl - ld;
-    s_ld[tid] = ld;
+    S.gb[tid] = a.digit_base[tid] + (wx_u32)excl - ld;
+    S.ld[tid] = ld;
   }
-  __syncthreads();
+}
+
+// Keys into digit order in LDS; pos[i] keeps each key's tile-local slot
+// (the payload follows through the same slots).
+template <int KIND, bool ASC>
+__device__ __forceinline__ void wx_rs_scatter(const WxRadixPassArgs &a, WxRsShared &S, wx_i64 wb,
+                                              const wx_u32 (&x)[WX_RS_ITEMS], const wx_u32 (&rk)[WX_RS_ITEMS],
+                                              wx_u32 (&pos)[WX_RS_ITEMS], wx_u32 *s_k) {
+  const int wave = threadIdx.x >> 6;
 #pragma unroll
   for (int i = 0; i < WX_RS_ITEMS; ++i) {
+    wx_u32 p = 0u;
     if (wb + (wx_i64)i * 64 < a.n) {
-      const wx_u32 d = (wx_rs_key(x[i], a.kind, a.ascending) >> a.shift) & 255u;
-      const wx_u32 pos = s_ld[d] + s_wc[wave][d] + rk[i];
-      s_k[pos] = x[i];
-      if (PAY) s_v[pos] = v[i];
+      const wx_u32 d = (wx_rs_key_t<KIND, ASC>(x[i]) >> a.shift) & 255u;
+      p = S.ld[d] + S.wc[wave][d] + rk[i];
+      s_k[p] = x[i];
     }
+    pos[i] = p;
   }
-  __syncthreads();
-  const wx_i64 rem = a.n - tb;
-  const int tile_n = rem < WX_RS_TILE ? (int)rem : WX_RS_TILE;
+}
+
+// LDS -> output: consecutive lanes write consecutive slots of a digit's run;
+// gdst[j] keeps the destination of slot j * WX_RS_BLOCK + tid for the payload.
+template <int KIND, bool ASC>
+__device__ __forceinline__ void wx_rs_store(const WxRadixPassArgs &a, const WxRsShared &S, int tile_n,
+                                            const wx_u32 *s_k, wx_u32 (&gdst)[WX_RS_ITEMS]) {
 #pragma unroll
   for (int j = 0; j < WX_RS_ITEMS; ++j) {
-    const int pos = j * WX_RS_BLOCK + tid;
+    const int pos = j * WX_RS_BLOCK + threadIdx.x;
+    gdst[j] = 0u;
     if (pos < tile_n) {
       const wx_u32 xk = s_k[pos];
-      const wx_u32 d = (wx_rs_key(xk, a.kind, a.ascending) >> a.shift) & 255u;
-      wx_u32 g = s_gb[d] + (wx_u32)pos;
+      const wx_u32 d = (wx_rs_key_t<KIND, ASC>(xk) >> a.shift) & 255u;
+      wx_u32 g = S.gb[d] + (wx_u32)pos;
       if (WX_RS_DIAG_NO_LOOKBACK) g = (wx_u32)min((wx_i64)g, a.n - 1);
       a.dst_k[g] = xk;
-      if (PAY) a.dst_v[g] = s_v[pos];
+      gdst[j] = g;
     }
   }
 }
 
-extern "C" __global__ __launch_bounds__(WX_RS_BLOCK) void wx_radix_pass_k(WxRadixPassArgs a) {
-  __shared__ wx_u32 s_k[WX_RS_TILE];
-  wx_radix_pass_impl<false>(a, s_k, nullptr);
+// The payload follows its key: the same LDS slots, the same destinations.
+__device__ __forceinline__ void wx_rs_payload(const WxRadixPassArgs &a, int tile_n, wx_i64 wb,
+                                              const wx_u32 (&v)[WX_RS_ITEMS], const wx_u32 (&pos)[WX_RS_ITEMS],
+                                              const wx_u32 (&gdst)[WX_RS_ITEMS], wx_u32 *s_k) {
+  __syncthreads();  // every key read out of s_k
+#pragma unroll
+  for (int i = 0; i < WX_RS_ITEMS; ++i)
+    if (wb + (wx_i64)i * 64 < a.n) s_k[pos[i]] = v[i];
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < WX_RS_ITEMS; ++j) {
+    const int p = j * WX_RS_BLOCK + threadIdx.x;
+    if (p < tile_n) a.dst_v[gdst[j]] = s_k[p];
+  }
 }
 
-extern "C" __global__ __launch_bounds__(WX_RS_BLOCK) void wx_radix_pass_kv(WxRadixPassArgs a) {
-  __shared__ wx_u32 s_k[WX_RS_TILE];
-  __shared__ wx_u32 s_v[WX_RS_TILE];
-  wx_radix_pass_impl<true>(a, s_k, s_v);
-}
+// One tile per workgroup, several workgroups per CU hiding each other's
+// latencies.  (A persistent variant that loaded the next tile during this
+// one's look-back needed 161 VGPRs, ran one workgroup per CU and took 33 ms
+// per 1e9 keys against 20.7 ms here: profiles/r01/bench_sort_variants.txt.)
+template <bool PAY, int KIND, bool ASC>
+__device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) S.tk[0] = atomicAdd(&a.ctl[0], 1u);
+  for (int i = tid; i < WX_RS_WAVES * 256; i += WX_RS_BLOCK) {
+    (&S.wc[0][0])[i] = 0u;
+#if WX_RS_MATCH_LDS
+    (&S.peers[0][0])[i] = 0ull;
 #endif
+  }
+  __syncthreads();
+  const wx_u32 tile = S.tk[0];
+  const wx_i64 tb = (wx_i64)tile * WX_RS_TILE;
+  const wx_i64 wb = tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane;
+  const int tile_n = a.n - tb < WX_RS_TILE ? (int)(a.n - tb) : WX_RS_TILE;
+  wx_u32 x[WX_RS_ITEMS], v[WX_RS_ITEMS], rk[WX_RS_ITEMS], pos[WX_RS_ITEMS], gdst[WX_RS_ITEMS];
+  wx_rs_load<PAY>(a, wb, tb + WX_RS_TILE <= a.n, x, v);
+  wx_rs_rank<KIND, ASC>(a, S, wb, x, rk);
+  __syncthreads();
+  wx_rs_digits(a, S, tile);
+  __syncthreads();
+  wx_rs_scatter<KIND, ASC>(a, S, wb, x, rk, pos, s_k);
+  __syncthreads();
+  wx_rs_store<KIND, ASC>(a, S, tile_n, s_k, gdst);
+  if (PAY) wx_rs_payload(a, tile_n, wb, v, pos, gdst, s_k);
+}
+
+#define WX_RS_TILEK(NAME, PAY, KIND, ASC)                                               \
+  extern "C" __global__ __launch_bounds__(WX_RS_BLOCK) void NAME(WxRadixPassArgs a) {   \
+    __shared__ WxRsShared S;                                                            \
+    __shared__ wx_u32 s_k[WX_RS_TILE];                                                  \
+    wx_radix_tile_impl<PAY, KIND, ASC>(a, S, s_k);                                      \
+  }
+WX_RS_TILEK(wx_radix_tile_k_f_a, false, 0, true)
+WX_RS_TILEK(wx_radix_tile_k_f_d, false, 0, false)
+WX_RS_TILEK(wx_radix_tile_k_i_a, false, 1, true)
+WX_RS_TILEK(wx_radix_tile_k_i_d, false, 1, false)
+WX_RS_TILEK(wx_radix_tile_kv_f_a, true, 0, true)
+WX_RS_TILEK(wx_radix_tile_kv_f_d, true, 0, false)
+WX_RS_TILEK(wx_radix_tile_kv_i_a, true, 1, true)
+WX_RS_TILEK(wx_radix_tile_kv_i_d, true, 1, false)
+#endif
+

@@ -477,9 +477,21 @@ std::vector<float> WarpDB::query_sql(const std::string &sql) {
   throw_on(wx_project_filter(&v.table, sel_c.c_str(), cond.c_str(), &L, WX_MODE_COMPACT, static_cast<float *>(dv.ptr),
                              nullptr, 0, 0, nullptr, &count, err, sizeof(err)),
            err);
-  if (ob || ast.distinct) {
-    if (ob && !same_expr(ob, sel))
-      throw std::runtime_error("ORDER BY a different expression needs LIMIT + OFFSET <= 32");
+  if (ob && !same_expr(ob, sel)) {
+    // ORDER BY another expression: its values at the same rows (same WHERE,
+    // same ascending row order) are the keys of a keyed sort that carries the
+    // SELECT values along (the pairs the reference builds, src/warpdb.cpp:470-476)
+    if (ast.distinct) throw std::runtime_error("DISTINCT with ORDER BY a different expression is not supported");
+    DeviceBuffer dk(table_.device, sizeof(float) * static_cast<size_t>(n ? n : 1));
+    int64_t kcount = 0;
+    throw_on(wx_project_filter(&v.table, ob->to_cuda_expr().c_str(), cond.c_str(), &L, WX_MODE_COMPACT,
+                               static_cast<float *>(dk.ptr), nullptr, 0, 0, nullptr, &kcount, err, sizeof(err)),
+             err);
+    if (kcount != count) throw std::runtime_error("ORDER BY rows differ from SELECT rows");
+    throw_on(wx_sort_by_key(static_cast<float *>(dk.ptr), static_cast<float *>(dv.ptr), count,
+                            ast.order_by->ascending ? 1 : 0, &L, err, sizeof(err)),
+             err);
+  } else if (ob || ast.distinct) {
     const bool asc = ob ? ast.order_by->ascending : true;
     throw_on(wx_sort_float(static_cast<float *>(dv.ptr), count, asc ? 1 : 0, &L, err, sizeof(err)), err);
   }
