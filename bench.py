@@ -43,6 +43,9 @@ WORKLOADS = {
     # WarpDB::query's own contract (src/warpdb.cpp:243-256): dense float[N],
     # 0.0f where WHERE fails, written in the same pass
     "dense": ("price * quantity WHERE price > 15", "wx_project_dense"),
+    # ORDER BY without LIMIT (query_sql): the projection, then the radix sort
+    # (jit_sort_float, src/jit.cpp:283-307); roofline over the sort's kernels
+    "sort": ("SELECT price FROM t ORDER BY price", "wx_radix_hist + wx_radix_tile_k_f_a"),
 }
 
 
@@ -56,6 +59,23 @@ def parse():
     p.add_argument("--cpu-sample", type=float, default=5e7, help="rows for the CPU baseline sample")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
+
+
+def cpu_sort_baseline(sample: int):
+    """ORDER BY on the host: the sample's values stable-sorted by numpy on one
+    core (the reference's own sort is a one-thread GPU bubble sort,
+    src/jit.cpp:283-307, with no CPU counterpart)."""
+    import numpy as np
+
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import synth  # noqa: E402
+
+    v = synth.c2_table(sample)["price"]
+    t0 = time.perf_counter()
+    np.sort(v, kind="stable")
+    dt = time.perf_counter() - t0
+    return {"value": round(sample / dt, 1), "unit": "rows/s", "cores": 1, "kind": "port",
+            "sample": f"{sample} synthetic price values, numpy stable sort (radix for float32) on one core, {dt:.2f} s"}
 
 
 def cpu_baseline(query: str, sample: int):
@@ -169,6 +189,13 @@ def main():
         def step(Lx):
             wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", Lx, wx.MODE_DENSE_FILL,
                               out_v.data_ptr(), 0, 4, 0)
+    elif args.workload == "sort":
+        out_v = torch.empty(n, dtype=torch.float32, device="cuda")
+
+        def step(Lx):
+            wx.project_filter(table, "price[idx]", None, L, wx.MODE_COMPACT, out_v.data_ptr(), 0, 4, 0,
+                              d_count=counts.data_ptr())
+            wx.sort_float(out_v.data_ptr(), n, True, Lx)  # synchronous, as jit_sort_float
     elif args.workload == "sum":
         res = torch.zeros(2, dtype=torch.float64, device="cuda")
 
@@ -225,6 +252,8 @@ def main():
         kern_avg_ms = km.item()
     else:
         kern_avg_ms = kern_ms / max(1, launches)
+    if args.workload == "sort":  # the sort's kernels as one unit: per step, not per launch
+        kern_avg_ms *= launches / max(1, args.steps)
 
     # algorithmic bytes per launch of the dominant kernel
     passing = int(counts.item()) if args.workload in ("project",) else None
@@ -234,10 +263,14 @@ def main():
         bytes_per_launch = n * 4
     elif args.workload == "dense":
         bytes_per_launch = n * 12
+    elif args.workload == "sort":  # histogram read + 4 passes of read + write
+        bytes_per_launch = n * (4 + 4 * 8)
     else:
         bytes_per_launch = n * 8
     achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
     read_bytes = n * (4 if args.workload in ("sum", "topk") else 8)
+    if args.workload == "sort":
+        read_bytes = n * (4 + 4 * 4)
 
     total_rows = n * world * args.steps
     value = total_rows / elapsed
@@ -252,8 +285,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         q = "price * quantity WHERE price > 15" if args.workload in ("project", "dense") else {
-            "sum": "price * 0.9 WHERE price > 20", "group": "price", "topk": "price"}[args.workload]
-        cpu = cpu_baseline(q, int(args.cpu_sample))
+            "sum": "price * 0.9 WHERE price > 20", "group": "price", "topk": "price", "sort": "price"}[args.workload]
+        cpu = cpu_sort_baseline(int(args.cpu_sample)) if args.workload == "sort" else cpu_baseline(q, int(args.cpu_sample))
 
     if rank == 0:
         line = {

@@ -157,6 +157,31 @@ def test_cpp_frontend_binary():
     assert "frontend_test: all passed" in r.stdout
 
 
+def test_host_code_under_asan_ubsan():
+    # tests/cpp/sanitize_test.cpp: the front end on random token soup and deep
+    # nesting, the parallel CSV parser against a sequential reading, built with
+    # -fsanitize=address,undefined (any report fails the run)
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "-C", os.path.join(root, "tests", "cpp"), "sanitize_test"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:halt_on_error=1", UBSAN_OPTIONS="halt_on_error=1")
+    r = subprocess.run([os.path.join(root, "tests", "cpp", "bin", "sanitize_test")], capture_output=True, text=True,
+                       cwd=root, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "sanitize_test: all passed" in r.stdout
+
+
+def test_parser_limits():
+    with pytest.raises(RuntimeError, match="nested too deeply"):
+        pw.lower_expression("(" * 10_000 + "1" + ")" * 10_000)
+    assert pw.lower_expression("(" * 100 + "price" + ")" * 100) == "price[idx]"
+    with pytest.raises(RuntimeError, match="LIMIT value out of range"):
+        pw.parse_query_summary("SELECT price FROM t LIMIT 99999999999")
+
+
 def _libc():
     import ctypes
 

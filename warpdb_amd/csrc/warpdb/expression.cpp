@@ -192,6 +192,11 @@ class Parser {
       ++i_;
       if (!accept_op("(")) return std::make_unique<VariableNode>(tok.value);
       std::vector<ASTNodePtr> args;
+      if (++depth_ > kMaxDepth) throw std::runtime_error("Expression nested too deeply");
+      struct Leave {
+        int &d;
+        ~Leave() { --d; }
+      } leave{depth_};
       if (!accept_op(")")) {
         do {
           args.push_back(additive());
@@ -211,17 +216,33 @@ class Parser {
       return std::make_unique<AggregationNode>(at, std::move(inner));
     }
     if (accept_op("(")) {
+      // the reference recurses without bound; a deep enough nest would
+      // overflow the caller's stack, so nesting is capped
+      if (++depth_ > kMaxDepth) throw std::runtime_error("Expression nested too deeply");
       ASTNodePtr n = additive();
+      --depth_;
       if (!accept_op(")")) throw std::runtime_error("Expected ')'");
       return n;
     }
     throw std::runtime_error(std::string("Unexpected token (") + type_name(tok.type) + ": " + tok.value + ")");
   }
 
+  static constexpr int kMaxDepth = 256;
   const std::vector<Token> &t_;
   size_t i_ = 0;
+  int depth_ = 0;
   bool aggs_;
 };
+
+// LIMIT / OFFSET count: std::stoi as the reference (src/expression.cpp:509,
+// 520), but a count beyond int is a query error, not std::out_of_range.
+int count_value(const std::string &text, const char *clause) {
+  try {
+    return std::stoi(text);
+  } catch (const std::out_of_range &) {
+    throw std::runtime_error(std::string(clause) + " value out of range: " + text);
+  }
+}
 
 std::vector<Token> slice(const std::vector<Token> &t, size_t a, size_t b) {
   std::vector<Token> s(t.begin() + static_cast<long>(a), t.begin() + static_cast<long>(b));
@@ -399,12 +420,12 @@ QueryAST parse_query(const std::vector<Token> &tokens) {
       ++pos;
       if (pos >= end || tokens[pos].type != TokenType::Number)
         throw std::runtime_error("Expected numeric value after LIMIT" + where_at(at(pos)));
-      q.limit = LimitClause{std::stoi(tokens[pos++].value)};
+      q.limit = LimitClause{count_value(tokens[pos++].value, "LIMIT")};
     } else if (is_kw(pos, "OFFSET") && !q.offset) {
       ++pos;
       if (pos >= end || tokens[pos].type != TokenType::Number)
         throw std::runtime_error("Expected numeric value after OFFSET");
-      q.offset = OffsetClause{std::stoi(tokens[pos++].value)};
+      q.offset = OffsetClause{count_value(tokens[pos++].value, "OFFSET")};
     }
   }
   if (pos != end) throw std::runtime_error("Unexpected token in query near: " + tokens[pos].value);
