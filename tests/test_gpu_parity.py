@@ -548,6 +548,18 @@ def test_sort_pairs_radix_stable(n, span):
         assert np.array_equal(tv.cpu().numpy(), pos[order])
 
 
+@pytest.mark.parametrize("n", [3, 10241, 400_007])
+def test_sort_float_unaligned_view(n):
+    # a sort of a tensor view 4 bytes into its allocation (scalar histogram
+    # loads); the element before the view must stay untouched
+    v = _sort_input(n, 31)
+    buf = torch.full((n + 1,), -123.0, dtype=torch.float32, device="cuda")
+    buf[1:].copy_(torch.from_numpy(v))
+    wx.sort_float(buf[1:].data_ptr(), n, False, launch())
+    assert np.array_equal(bits(buf[1:].cpu().numpy()), bits(v[np.argsort(-v, kind="stable")]))
+    assert buf[0].item() == -123.0
+
+
 @pytest.mark.parametrize("n", [1, 12289, 1_000_003])
 @pytest.mark.parametrize("sort", ["radix", "bitonic"])
 def test_sort_by_key_stable(n, sort, monkeypatch):

@@ -189,8 +189,7 @@ struct WxRadixHistArgs {
   const wx_u32 *src;
   wx_i64 n;
   wx_u32 *hist;  // [4][256], zeroed by the host
-  int kind;      // 0 float values, 1 int keys
-  int ascending;
+  int aligned;   // src is 16-byte aligned
 };
 
 struct WxRadixPassArgs {

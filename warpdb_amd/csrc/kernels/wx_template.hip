@@ -1783,72 +1783,6 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApply
 #define WX_RS_FLAG_P (2ull << 56)
 #define WX_RS_VAL_MASK ((1ull << 56) - 1ull)
 
-__device__ __forceinline__ wx_u32 wx_rs_key(wx_u32 x, int kind, int asc) {
-  wx_u32 r;
-  if (kind == 0) {
-    r = wx::f2ord(__uint_as_float(x));
-    if (r == 0u) return 0xffffffffu;  // NaN last in either direction
-  } else {
-    r = x ^ 0x80000000u;
-  }
-  return asc ? r : ~r;
-}
-
-#ifndef WX_RS_HCOPIES
-#define WX_RS_HCOPIES 8  // LDS histogram copies, picked by lane % copies: few-valued digits conflict 8x less
-#endif
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist(WxRadixHistArgs a) {
-  __shared__ wx_u32 h[4 * 256 * WX_RS_HCOPIES];  // [digit][bin][copy]
-  for (int i = threadIdx.x; i < 4 * 256 * WX_RS_HCOPIES; i += WX_BLOCK) h[i] = 0u;
-  __syncthreads();
-  const int lane = threadIdx.x & 63;
-  const int copy = lane % WX_RS_HCOPIES;
-  const wx_i64 span = (wx_i64)WX_BLOCK * 8;
-  for (wx_i64 base = (wx_i64)blockIdx.x * span; base < a.n; base += (wx_i64)gridDim.x * span) {
-    wx_u32 x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const wx_i64 i = base + (wx_i64)u * WX_BLOCK + threadIdx.x;
-      x[u] = i < a.n ? wx::ldv(a.src + i) : 0u;
-    }
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const wx_i64 i = base + (wx_i64)u * WX_BLOCK + threadIdx.x;
-      if (i < a.n) {
-        const wx_u32 k = wx_rs_key(x[u], a.kind, a.ascending);
-        const wx_u64 act = __builtin_amdgcn_ballot_w64(true);
-        const int first = __builtin_ctzll(act);
-#pragma unroll
-        for (int p = 0; p < 4; ++p) {
-          const wx_u32 d = (k >> (8 * p)) & 255u;
-          const wx_u32 d0 = __builtin_amdgcn_readfirstlane(d);
-          if (__builtin_amdgcn_ballot_w64(d != d0) == 0ull) {
-            if (lane == first) atomicAdd(&h[(p * 256 + d0) * WX_RS_HCOPIES], (wx_u32)__builtin_popcountll(act));
-          } else {
-            atomicAdd(&h[(p * 256 + d) * WX_RS_HCOPIES + copy], 1u);
-          }
-        }
-      }
-    }
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < 4 * 256; i += WX_BLOCK) {
-    wx_u32 c = 0u;
-#pragma unroll
-    for (int j = 0; j < WX_RS_HCOPIES; ++j) c += h[i * WX_RS_HCOPIES + j];
-    if (c) atomicAdd(&a.hist[i], c);
-  }
-}
-
-#ifndef WX_RS_DIAG_NO_LOOKBACK
-#define WX_RS_DIAG_NO_LOOKBACK 0  // diagnostic: every tile takes its offset as 0 (results invalid)
-#endif
-#ifndef WX_RS_MATCH_LDS
-// Digit peers of a key by one ds_or_b64 of the lane's bit into a per-digit
-// LDS mask (then read back and cleared): 3 LDS operations per key instead of
-// eight ballots and ~70 VALU instructions.  0 selects the ballot form.
-#define WX_RS_MATCH_LDS 1
-#endif
 
 // Order key with the direction and key kind known at compile time.
 template <int KIND, bool ASC>
@@ -1862,6 +1796,89 @@ __device__ __forceinline__ wx_u32 wx_rs_key_t(wx_u32 x) {
   }
   return ASC ? r : ~r;
 }
+
+#ifndef WX_RS_HCOPIES
+#define WX_RS_HCOPIES 8  // LDS histogram copies, picked by lane % copies: few-valued digits conflict 8x less
+#endif
+#ifndef WX_RS_HUNROLL
+#define WX_RS_HUNROLL 4  // 16-byte loads in flight per thread (64 B): the kernel is latency-bound below that
+#endif
+template <int KIND, bool ASC>
+__device__ __forceinline__ void wx_rs_count(wx_u32 *h, wx_u32 x, int lane, int copy) {
+  const wx_u32 k = wx_rs_key_t<KIND, ASC>(x);
+  const wx_u64 act = __builtin_amdgcn_ballot_w64(true);
+  const int first = __builtin_ctzll(act);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) {
+    const wx_u32 d = (k >> (8 * p)) & 255u;
+    const wx_u32 d0 = __builtin_amdgcn_readfirstlane(d);
+    if (__builtin_amdgcn_ballot_w64(d != d0) == 0ull) {
+      if (lane == first) atomicAdd(&h[(p * 256 + d0) * WX_RS_HCOPIES], (wx_u32)__builtin_popcountll(act));
+    } else {
+      atomicAdd(&h[(p * 256 + d) * WX_RS_HCOPIES + copy], 1u);
+    }
+  }
+}
+
+// All four digit histograms in one read: contiguous spans of 16-byte loads
+// (WX_RS_HUNROLL per thread) when the array is 16-byte aligned, scalar
+// loads otherwise; per-workgroup LDS counters, one global add per bin.
+template <int KIND, bool ASC>
+__device__ __forceinline__ void wx_radix_hist_impl(const WxRadixHistArgs &a) {
+  __shared__ wx_u32 h[4 * 256 * WX_RS_HCOPIES];  // [digit][bin][copy]
+  for (int i = threadIdx.x; i < 4 * 256 * WX_RS_HCOPIES; i += WX_BLOCK) h[i] = 0u;
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int copy = lane % WX_RS_HCOPIES;
+  if (a.aligned) {
+    typedef wx_u32 u4 __attribute__((ext_vector_type(4)));
+    const u4 *q = reinterpret_cast<const u4 *>(a.src);
+    const wx_i64 nq = a.n >> 2;
+    const wx_i64 span = (wx_i64)WX_BLOCK * WX_RS_HUNROLL;
+    for (wx_i64 base = (wx_i64)blockIdx.x * span; base < nq; base += (wx_i64)gridDim.x * span) {
+      u4 v[WX_RS_HUNROLL];
+#pragma unroll
+      for (int u = 0; u < WX_RS_HUNROLL; ++u) {
+        const wx_i64 i = base + (wx_i64)u * WX_BLOCK + threadIdx.x;
+        if (i < nq) v[u] = wx::ldv(q + i);
+      }
+#pragma unroll
+      for (int u = 0; u < WX_RS_HUNROLL; ++u) {
+        if (base + (wx_i64)u * WX_BLOCK + threadIdx.x < nq) {
+          wx_rs_count<KIND, ASC>(h, v[u].x, lane, copy);
+          wx_rs_count<KIND, ASC>(h, v[u].y, lane, copy);
+          wx_rs_count<KIND, ASC>(h, v[u].z, lane, copy);
+          wx_rs_count<KIND, ASC>(h, v[u].w, lane, copy);
+        }
+      }
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) wx_rs_count<KIND, ASC>(h, a.src[nq * 4 + threadIdx.x], lane, copy);
+  } else {
+    for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.n; i += (wx_i64)gridDim.x * WX_BLOCK)
+      wx_rs_count<KIND, ASC>(h, wx::ldv(a.src + i), lane, copy);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 4 * 256; i += WX_BLOCK) {
+    wx_u32 c = 0u;
+#pragma unroll
+    for (int j = 0; j < WX_RS_HCOPIES; ++j) c += h[i * WX_RS_HCOPIES + j];
+    if (c) atomicAdd(&a.hist[i], c);
+  }
+}
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_f_a(WxRadixHistArgs a) { wx_radix_hist_impl<0, true>(a); }
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_f_d(WxRadixHistArgs a) { wx_radix_hist_impl<0, false>(a); }
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_i_a(WxRadixHistArgs a) { wx_radix_hist_impl<1, true>(a); }
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_i_d(WxRadixHistArgs a) { wx_radix_hist_impl<1, false>(a); }
+
+#ifndef WX_RS_DIAG_NO_LOOKBACK
+#define WX_RS_DIAG_NO_LOOKBACK 0  // diagnostic: every tile takes its offset as 0 (results invalid)
+#endif
+#ifndef WX_RS_MATCH_LDS
+// Digit peers of a key by one ds_or_b64 of the lane's bit into a per-digit
+// LDS mask (then read back and cleared): 3 LDS operations per key instead of
+// eight ballots and ~70 VALU instructions.  0 selects the ballot form.
+#define WX_RS_MATCH_LDS 1
+#endif
 
 struct WxRsShared {
   wx_u32 wc[WX_RS_WAVES][256];  // per-wave digit counts, then their exclusive prefix over the waves
