@@ -64,8 +64,14 @@ def test_query_dense_and_compact_vs_oracle(tmp_path):
     s, c = db.query_sum("price * 0.9 WHERE price > 20")
     rs, rc = ora.reduce_sum(ora.HostTable(cols), "price * 0.9", "price > 20")
     assert c == rc and s == rs
-    # multi-GPU paths (every visible GPU; one on the test box)
+    # multi-GPU paths (every visible GPU; one on the test box), also with the
+    # host pipeline cut into many ragged chunks
     assert db.query_multi_gpu("price * quantity WHERE price > 15") == dense.tolist()
+    os.environ["WARPDB_HOST_CHUNK_ROWS"] = "4097"
+    try:
+        assert db.query_multi_gpu("price * quantity WHERE price > 15") == dense.tolist()
+    finally:
+        del os.environ["WARPDB_HOST_CHUNK_ROWS"]
     ms, mc = db.query_multi_gpu_sum("price * 0.9 WHERE price > 20")
     assert mc == rc and ms == rs
     chunked = pw().WarpDB.query_multi_gpu_csv(str(path), "price * quantity WHERE price > 15", 7_777)

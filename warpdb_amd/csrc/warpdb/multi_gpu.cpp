@@ -10,9 +10,14 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
+#include <cstdio>
+#include <condition_variable>
 #include <cstring>
 #include <exception>
 #include <future>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <thread>
@@ -88,18 +93,40 @@ void run_per_device(const std::vector<ShardRange> &shards, F &&fn) {
     if (e) std::rethrow_exception(e);
 }
 
-// One long-lived stream per device: the execution layer keys its workspaces
-// by (device, stream), so reusing the streams reuses the workspaces.
-hipStream_t device_stream(int device) {
+// Long-lived streams per device (role 0: uploads + kernels, role 1:
+// downloads): the execution layer keys its workspaces by (device, stream),
+// so reusing the streams reuses the workspaces.
+hipStream_t device_stream(int device, int role = 0) {
   static std::mutex mu;
-  static std::vector<hipStream_t> streams;
+  static std::vector<hipStream_t> streams[2];
   std::lock_guard<std::mutex> lk(mu);
-  if ((int)streams.size() <= device) streams.resize(device + 1, nullptr);
-  if (!streams[device]) {
+  auto &v = streams[role];
+  if ((int)v.size() <= device) v.resize(device + 1, nullptr);
+  if (!v[device]) {
     DevGuard g(device);
-    hip_ok(hipStreamCreateWithFlags(&streams[device], hipStreamNonBlocking), "hipStreamCreate");
+    hip_ok(hipStreamCreateWithFlags(&v[device], hipStreamNonBlocking), "hipStreamCreate");
   }
-  return streams[device];
+  return v[device];
+}
+
+// Per-device scratch HBM for the host-resident pipeline, kept across calls
+// and grown on demand: hipMalloc + hipFree of a 1.2 GB shard took 7-14 ms of
+// a 31 ms query (1e8 rows, 1 GPU).  The lock is held for a whole call, so
+// concurrent host callers take turns per device.
+struct Scratch {
+  std::mutex mu;
+  DeviceBuffer buf;
+  size_t bytes = 0;
+};
+Scratch &scratch_for(int device) {
+  static std::mutex mu;
+  // never destroyed: freeing HBM from a static destructor would run after
+  // the HIP runtime's own teardown
+  static auto *all = new std::map<int, std::unique_ptr<Scratch>>();
+  std::lock_guard<std::mutex> lk(mu);
+  auto &p = (*all)[device];
+  if (!p) p.reset(new Scratch);
+  return *p;
 }
 
 struct Comms {
@@ -184,36 +211,157 @@ std::vector<float> run_multi_gpu_jit_host(const HostTable &host, const std::stri
   const int64_t n = host.num_rows();
   auto shards = plan_shards(n, device_count());
   // The host result (4 B/row, first-touch bound) is allocated on its own
-  // thread while the devices upload and compute; D2H waits for it.
+  // thread while the devices upload and compute; downloads wait for it.
   std::vector<float> result;
   std::promise<void> ready;
   std::shared_future<void> result_ready = ready.get_future().share();
-  std::thread alloc([&] {
+  auto make_result = [&] {
     try {
       result = host_result(static_cast<size_t>(n));
       ready.set_value();
     } catch (...) {
       ready.set_exception(std::current_exception());
     }
+  };
+  const bool serial_alloc = std::string(std::getenv("WARPDB_HOST_ALLOC") ? std::getenv("WARPDB_HOST_ALLOC") : "serial") ==
+                            "serial";
+  if (serial_alloc) make_result();
+  std::thread alloc([&] {
+    if (!serial_alloc) make_result();
   });
   struct Join {
     std::thread &t;
     ~Join() { t.join(); }
   } join{alloc};
+  // Per device, a chunked pipeline over its shard: this thread uploads chunk
+  // c and runs the dense kernel on it (stream 0) while a second thread
+  // downloads chunk c - 1 (stream 1), so the two PCIe directions overlap
+  // (the reference uploads, runs and downloads each shard in turn,
+  // src/multi_gpu_utils.cpp:34-58).  Chunks are multiples of 4 rows, so the
+  // chunk views keep the columns' 16-byte alignment.
+  const int64_t chunk_rows = std::max<int64_t>(
+      4, (std::atoll(std::getenv("WARPDB_HOST_CHUNK_ROWS") ? std::getenv("WARPDB_HOST_CHUNK_ROWS") : "16777216") + 3) &
+             ~int64_t(3));
+  const bool debug = std::getenv("WARPDB_DEBUG") != nullptr;
+  const auto t_start = std::chrono::steady_clock::now();
+  auto stamp = [&](const char *what, int dev, int64_t c) {
+    if (!debug) return;
+    const double ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_start).count();
+    std::fprintf(stderr, "[multi_gpu] %8.3f ms dev %d chunk %lld %s\n", ms, dev, (long long)c, what);
+  };
   run_per_device(shards, [&](size_t, const ShardRange &r) {
-    hipStream_t s = device_stream(r.device);
-    Shard sh = upload_shard(host, r.device, r.begin, r.end, s);
-    DeviceBuffer out(r.device, sizeof(float) * static_cast<size_t>(r.end - r.begin));
-    WxTableView v(sh.table);
-    wx_launch L = sync_launch(r.device, s);
-    L.flags = 0;
-    char err[8192];
-    throw_on(wx_project_filter(&v.table, expr_cuda.c_str(), cond_cuda.c_str(), &L, WX_MODE_DENSE_FILL,
-                               static_cast<float *>(out.ptr), nullptr, 0, 0, nullptr, nullptr, err, sizeof(err)),
-             err);
-    result_ready.get();
-    copy_d2h(r.device, s, result.data() + r.begin, out.ptr, sizeof(float) * static_cast<size_t>(r.end - r.begin));
-    throw_on(wx_check(&L, err, sizeof(err)), err);
+    hipStream_t s = device_stream(r.device, 0), s2 = device_stream(r.device, 1);
+    const int64_t rows = r.end - r.begin;
+    const int64_t n_chunks = (rows + chunk_rows - 1) / chunk_rows;
+    // device copies of the numeric columns of this shard and its output, in
+    // the device's scratch HBM (256-byte aligned slices)
+    Scratch &scr = scratch_for(r.device);
+    std::lock_guard<std::mutex> scr_lock(scr.mu);
+    std::vector<const char *> src;
+    std::vector<size_t> width, offset;
+    size_t total = 0;
+    auto slice = [&](size_t bytes) {
+      const size_t at = total;
+      total += (bytes + 255) & ~size_t(255);
+      return at;
+    };
+    for (const auto &c : host.columns) {
+      const size_t w = (c.type == DataType::Int64 || c.type == DataType::Float64) ? 8 : 4;
+      width.push_back(w);
+      src.push_back(c.type == DataType::String
+                        ? nullptr
+                        : static_cast<const char *>(std::visit([](auto &&v) -> const void * { return v.data(); }, c.data)));
+      offset.push_back(c.type == DataType::String ? 0 : slice(w * static_cast<size_t>(rows)));
+    }
+    const size_t out_off = slice(sizeof(float) * static_cast<size_t>(rows));
+    if (scr.bytes < total) {
+      scr.buf = DeviceBuffer();
+      scr.buf = DeviceBuffer(r.device, total);
+      scr.bytes = total;
+    }
+    char *base = static_cast<char *>(scr.buf.ptr);
+    float *out = reinterpret_cast<float *>(base + out_off);
+    stamp("device buffers", r.device, -1);
+    std::vector<hipEvent_t> done(static_cast<size_t>(n_chunks), nullptr);
+    for (auto &e : done) hip_ok(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+    struct Events {
+      std::vector<hipEvent_t> &v;
+      ~Events() {
+        for (auto e : v)
+          if (e) (void)hipEventDestroy(e);
+      }
+    } ev_guard{done};
+    std::mutex mu;
+    std::condition_variable cv;
+    int64_t recorded = 0;
+    bool failed = false;
+    std::exception_ptr d2h_err;
+    std::thread down([&] {
+      try {
+        DevGuard g(r.device);
+        result_ready.get();
+        stamp("result ready", r.device, -1);
+        for (int64_t c = 0; c < n_chunks; ++c) {
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return recorded > c || failed; });
+            if (failed) return;
+          }
+          hip_ok(hipStreamWaitEvent(s2, done[c], 0), "hipStreamWaitEvent");
+          const int64_t c0 = c * chunk_rows, cr = std::min(chunk_rows, rows - c0);
+          copy_d2h(r.device, s2, result.data() + r.begin + c0, out + c0, sizeof(float) * static_cast<size_t>(cr));
+          stamp("downloaded", r.device, c);
+        }
+      } catch (...) {
+        d2h_err = std::current_exception();
+      }
+    });
+    try {
+      char err[8192];
+      for (int64_t c = 0; c < n_chunks; ++c) {
+        const int64_t c0 = c * chunk_rows, cr = std::min(chunk_rows, rows - c0);
+        Table chunk;
+        chunk.num_rows = cr;
+        chunk.device = r.device;
+        for (size_t k = 0; k < host.columns.size(); ++k) {
+          const auto &hc = host.columns[k];
+          if (hc.type == DataType::String) {
+            chunk.columns.push_back({hc.name, hc.type, nullptr, cr});
+            continue;
+          }
+          char *dst = base + offset[k] + width[k] * static_cast<size_t>(c0);
+          copy_h2d(r.device, s, dst, src[k] + width[k] * static_cast<size_t>(r.begin + c0),
+                   width[k] * static_cast<size_t>(cr));
+          chunk.columns.push_back({hc.name, hc.type, dst, cr});
+        }
+        WxTableView v(chunk);
+        wx_launch L = sync_launch(r.device, s);
+        L.flags = 0;
+        throw_on(wx_project_filter(&v.table, expr_cuda.c_str(), cond_cuda.c_str(), &L, WX_MODE_DENSE_FILL, out + c0,
+                                   nullptr, 0, 0, nullptr, nullptr, err, sizeof(err)),
+                 err);
+        hip_ok(hipEventRecord(done[c], s), "hipEventRecord");
+        stamp("uploaded + launched", r.device, c);
+        {
+          std::lock_guard<std::mutex> lk(mu);
+          recorded = c + 1;
+        }
+        cv.notify_one();
+      }
+      wx_launch L = sync_launch(r.device, s);
+      throw_on(wx_check(&L, err, sizeof(err)), err);
+    } catch (...) {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        failed = true;
+      }
+      cv.notify_one();
+      down.join();
+      throw;
+    }
+    down.join();
+    if (d2h_err) std::rethrow_exception(d2h_err);
+    hip_ok(hipStreamSynchronize(s2), "hipStreamSynchronize");
   });
   result_ready.get();  // n == 0: no device ran
   return result;
