@@ -6,7 +6,7 @@ set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 O=$R/gpurun_out/refresh
 mkdir -p "$O"
-WL=${WL:-"project sum group topk"}
+WL=${WL:-"project dense sum group topk sort"}
 cd "$R"
 if [ -z "${SKIP_TESTS:-}" ]; then
   timeout -k 10 600 python3 -m pytest tests -m gpu -x -q > "$O/pytest_gpu.log" 2>&1
@@ -21,6 +21,7 @@ for W in $WL; do
 done
 if [ -n "${PMC:-}" ]; then
   for W in $WL; do
+    [ "$W" = sort ] && continue  # several kernels per step: no per-launch traffic
     timeout -k 10 700 bash "$R/tools/pmc_run.sh" "$W" > "$O/pmc_$W.log" 2>&1
   done
 fi

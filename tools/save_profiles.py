@@ -11,7 +11,8 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-K = {"project": "wx_project_compact", "sum": "wx_reduce_sum", "group": "wx_group_sum", "topk": "wx_topk_scan", "dense": "wx_project_dense"}
+K = {"project": "wx_project_compact", "sum": "wx_reduce_sum", "group": "wx_group_sum", "topk": "wx_topk_scan", "dense": "wx_project_dense",
+     "sort": "wx_radix_tile_k_f_a"}
 rnd = sys.argv[1]
 wls = sys.argv[2:] or list(K)
 out = os.path.join(ROOT, "profiles", rnd)
@@ -21,7 +22,7 @@ for w in wls:
     k = K[w]
     b = [json.loads(line) for line in open(os.path.join(go, "refresh", f"bench_{w}.log")) if line.startswith("{")][0]
     pmc_sum = os.path.join(go, f"pmc_{w}", "summary.json")
-    if os.path.exists(pmc_sum):
+    if os.path.exists(pmc_sum) and w != "sort":  # sort: several kernels per step, no per-launch traffic
         s = json.load(open(pmc_sum))
         k = b["roofline"]["kernel"] if b["roofline"]["kernel"] in s else k
         s = s[k]
