@@ -2110,8 +2110,13 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
   if (PAY) wx_rs_payload(a, tile_n, wb, v, pos, gdst, s_k);
 }
 
-#define WX_RS_TILEK(NAME, PAY, KIND, ASC)                                               \
-  extern "C" __global__ __launch_bounds__(WX_RS_BLOCK) void NAME(WxRadixPassArgs a) {   \
+#ifndef WX_RS_MINW
+// minimum waves per SIMD the register allocation must allow: 2 workgroups
+// per CU for the 512-thread key tiles (<= 128 VGPRs), 1 for 1024 threads
+#define WX_RS_MINW (WX_RS_BLOCK <= 512 ? 2 * WX_RS_BLOCK / 256 : WX_RS_BLOCK / 256)
+#endif
+#define WX_RS_TILEK(NAME, PAY, KIND, ASC)                                                        \
+  extern "C" __global__ __launch_bounds__(WX_RS_BLOCK, WX_RS_MINW) void NAME(WxRadixPassArgs a) { \
     __shared__ WxRsShared S;                                                            \
     __shared__ wx_u32 s_k[WX_RS_TILE];                                                  \
     wx_radix_tile_impl<PAY, KIND, ASC>(a, S, s_k);                                      \
