@@ -169,6 +169,14 @@ wx_status wx_sort_float(float *d_vals, int64_t count, int32_t ascending, const w
 wx_status wx_sort_by_key(float *d_keys, float *d_vals, int64_t count, int32_t ascending,
                          const wx_launch *launch, char *err, size_t errlen);
 
+/* ORDER BY .. LIMIT: as wx_sort_float / wx_sort_by_key, but only the first
+ * min(limit, count) positions are required to hold the sorted order (the
+ * rest of the buffers is left unspecified). */
+wx_status wx_sort_float_limit(float *d_vals, int64_t count, int64_t limit, int32_t ascending,
+                              const wx_launch *launch, char *err, size_t errlen);
+wx_status wx_sort_by_key_limit(float *d_keys, float *d_vals, int64_t count, int64_t limit,
+                               int32_t ascending, const wx_launch *launch, char *err, size_t errlen);
+
 /* Seeded synthetic column generator (counter-based, so every shard can
  * generate its own rows on the device):  h = splitmix64(row + seed * 0xD1B54A32D192ED03)
  *   kind 0: uniform float  lo + ((h >> 40) * 2^-24) * (hi - lo)   (float arithmetic)

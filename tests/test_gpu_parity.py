@@ -548,6 +548,26 @@ def test_sort_pairs_radix_stable(n, span):
         assert np.array_equal(tv.cpu().numpy(), pos[order])
 
 
+@pytest.mark.parametrize("data", ["uniform", "ties_nan"])
+@pytest.mark.parametrize("limit", [0, 1, 1000, 777_777, 5_000_000])
+def test_sort_limit_head_matches_full_sort(data, limit):
+    # ORDER BY .. LIMIT: the first `limit` positions equal the stable full
+    # sort's (uniform data takes the top-digit head path for small limits)
+    n = 3_000_017
+    v = synth.uniform_f32(n, 41, 0.0, 40.0) if data == "uniform" else _sort_input(n, 43)
+    pos = np.arange(n, dtype=np.float32)
+    k = min(limit, n)
+    for asc in (True, False):
+        order = np.argsort(v if asc else -v, kind="stable")[:k]
+        t = torch.from_numpy(v.copy()).cuda()
+        wx.sort_float_limit(t.data_ptr(), n, limit, asc, launch())
+        assert np.array_equal(bits(t[:k].cpu().numpy()), bits(v[order]))
+        tk = torch.from_numpy(v.copy()).cuda()
+        tv = torch.from_numpy(pos.copy()).cuda()
+        wx.sort_by_key_limit(tk.data_ptr(), tv.data_ptr(), n, limit, asc, launch())
+        assert np.array_equal(tv[:k].cpu().numpy(), pos[order])
+
+
 @pytest.mark.parametrize("n", [3, 10241, 400_007])
 def test_sort_float_unaligned_view(n):
     # a sort of a tensor view 4 bytes into its allocation (scalar histogram

@@ -59,3 +59,25 @@ for n in sizes:
                   f"{gb / med / 1e9:7.1f} GB/s (4 passes)  sorted={ok}", flush=True)
     del src, keys, buf, kb
     torch.cuda.empty_cache()
+
+# ORDER BY .. LIMIT k: the partial sort (top-digit head + full sort of it)
+n = sizes[-1]
+src = torch.empty(n, dtype=torch.float32, device="cuda")
+wx.fill_synthetic(src.data_ptr(), wx.FLOAT32, n, 1, 0, 0.0, 40.0, L)
+buf = torch.empty_like(src)
+os.environ["WARPDB_SORT"] = "radix"
+for k, asc in ((100, True), (100, False), (1_000_000, True), (1_000_000, False)):
+    ts = []
+    for r in range(4):
+        buf.copy_(src)
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        wx.sort_float_limit(buf.data_ptr(), n, k, asc, L)
+        torch.cuda.synchronize()
+        if r:
+            ts.append(time.perf_counter() - t0)
+    ts.sort()
+    ref = torch.sort(src, descending=not asc).values[:k]
+    ok = bool(torch.equal(buf[:k], ref))
+    print(f"limit    float  n={n:>11d}  k={k:>8d} {'asc ' if asc else 'desc'} {ts[len(ts) // 2] * 1e3:9.3f} ms  "
+          f"head correct={ok}", flush=True)

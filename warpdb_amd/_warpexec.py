@@ -49,6 +49,8 @@ EXPORTED_SYMBOLS = (
     "wx_sort_pairs",
     "wx_sort_float",
     "wx_sort_by_key",
+    "wx_sort_float_limit",
+    "wx_sort_by_key_limit",
     "wx_fill_synthetic",
     "wx_prepare",
     "wx_check",
@@ -118,6 +120,8 @@ def load() -> ctypes.CDLL:
         "wx_sort_pairs": [P, P, I64, I32, L, E, S],
         "wx_sort_float": [P, I64, I32, L, E, S],
         "wx_sort_by_key": [P, P, I64, I32, L, E, S],
+        "wx_sort_float_limit": [P, I64, I64, I32, L, E, S],
+        "wx_sort_by_key_limit": [P, P, I64, I64, I32, L, E, S],
         "wx_fill_synthetic": [P, I32, I64, U64, I32, D, D, I64, L, E, S],
         "wx_prepare": [T, I32, E, E, E, I32, L, E, S, E, S],
         "wx_check": [L, E, S],
@@ -288,6 +292,20 @@ def sort_by_key(d_keys: int, d_vals: int, count: int, ascending: bool, launch: W
     lib = load()
     err = _err()
     _check(lib.wx_sort_by_key(d_keys, d_vals, count, 1 if ascending else 0, ctypes.byref(launch), err, len(err)), err)
+
+
+def sort_float_limit(d_vals: int, count: int, limit: int, ascending: bool, launch: WxLaunch) -> None:
+    lib = load()
+    err = _err()
+    _check(lib.wx_sort_float_limit(d_vals, count, limit, 1 if ascending else 0, ctypes.byref(launch), err, len(err)),
+           err)
+
+
+def sort_by_key_limit(d_keys: int, d_vals: int, count: int, limit: int, ascending: bool, launch: WxLaunch) -> None:
+    lib = load()
+    err = _err()
+    _check(lib.wx_sort_by_key_limit(d_keys, d_vals, count, limit, 1 if ascending else 0, ctypes.byref(launch), err,
+                                    len(err)), err)
 
 
 def fill_synthetic(d_ptr: int, dtype: int, n: int, seed: int, kind: int, lo: float, hi: float,

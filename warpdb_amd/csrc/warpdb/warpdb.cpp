@@ -488,12 +488,20 @@ std::vector<float> WarpDB::query_sql(const std::string &sql) {
                                static_cast<float *>(dk.ptr), nullptr, 0, 0, nullptr, &kcount, err, sizeof(err)),
              err);
     if (kcount != count) throw std::runtime_error("ORDER BY rows differ from SELECT rows");
-    throw_on(wx_sort_by_key(static_cast<float *>(dk.ptr), static_cast<float *>(dv.ptr), count,
-                            ast.order_by->ascending ? 1 : 0, &L, err, sizeof(err)),
+    // with a LIMIT only the first OFFSET + LIMIT rows of the order are needed
+    throw_on(wx_sort_by_key_limit(static_cast<float *>(dk.ptr), static_cast<float *>(dv.ptr), count,
+                                  ast.limit ? std::min<int64_t>(count, off + lim) : count,
+                                  ast.order_by->ascending ? 1 : 0, &L, err, sizeof(err)),
              err);
+    if (ast.limit) count = std::min<int64_t>(count, off + lim);
   } else if (ob || ast.distinct) {
     const bool asc = ob ? ast.order_by->ascending : true;
-    throw_on(wx_sort_float(static_cast<float *>(dv.ptr), count, asc ? 1 : 0, &L, err, sizeof(err)), err);
+    const bool head_only = ob && !ast.distinct && ast.limit;  // DISTINCT needs every value
+    throw_on(wx_sort_float_limit(static_cast<float *>(dv.ptr), count,
+                                 head_only ? std::min<int64_t>(count, off + lim) : count, asc ? 1 : 0, &L, err,
+                                 sizeof(err)),
+             err);
+    if (head_only) count = std::min<int64_t>(count, off + lim);
   }
   result = download(dv.ptr, count, table_.device);
   if (ast.distinct) result.erase(std::unique(result.begin(), result.end()), result.end());
