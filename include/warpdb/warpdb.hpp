@@ -1,6 +1,7 @@
 // warpdb.hpp -- the WarpDB facade (drop-in for the reference's
 // include/warpdb.hpp:11-48) running on the MI355X execution layer.
 #pragma once
+#include <memory>
 #include <string>
 #include <utility>
 #include <vector>
@@ -10,6 +11,10 @@
 #include "expression.hpp"
 #include "jit.hpp"
 #include "json_loader.hpp"
+
+namespace warpdb {
+class ResidentShards;
+}
 
 class WarpDB {
  public:
@@ -56,4 +61,5 @@ class WarpDB {
   void lower(const std::string &query, std::string &expr_c, std::string &cond_c) const;
   Table table_;
   HostTable host_table_;
+  std::unique_ptr<warpdb::ResidentShards> shards_;  // query_multi_gpu*: built on first use
 };

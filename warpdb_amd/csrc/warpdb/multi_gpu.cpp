@@ -151,17 +151,19 @@ Comms &comms_for(int ndev) {
 
 }  // namespace
 
-std::pair<double, int64_t> run_multi_gpu_sum(const HostTable &host, const std::string &expr_cuda,
-                                             const std::string &cond_cuda) {
-  const int ndev = device_count();
-  auto shards = plan_shards(host.num_rows(), ndev);
+namespace {
+
+// SUM over shards already in HBM: one reduce per device, then one RCCL
+// all-reduce of {sum (f64), count (i64)} across the shards' devices.
+std::pair<double, int64_t> sum_over_shards(const std::vector<ShardRange> &shards, std::vector<Shard> &keep,
+                                           const std::string &expr_cuda, const std::string &cond_cuda,
+                                           const HostTable *upload_from) {
   if (shards.empty()) return {0.0, 0};
   std::vector<DeviceBuffer> outs(shards.size());
   std::vector<hipStream_t> streams(shards.size(), nullptr);
-  std::vector<Shard> keep(shards.size());
   run_per_device(shards, [&](size_t i, const ShardRange &r) {
     streams[i] = device_stream(r.device);
-    keep[i] = upload_shard(host, r.device, r.begin, r.end, streams[i]);
+    if (upload_from) keep[i] = upload_shard(*upload_from, r.device, r.begin, r.end, streams[i]);
     outs[i] = DeviceBuffer(r.device, 16);
     WxTableView v(keep[i].table);
     wx_launch L = sync_launch(r.device, streams[i]);
@@ -171,7 +173,6 @@ std::pair<double, int64_t> run_multi_gpu_sum(const HostTable &host, const std::s
                            sizeof(err)),
              err);
   });
-  // one all-reduce of {sum (f64), count (i64)} across the shards' devices
   const int nshard = static_cast<int>(shards.size());
   Comms &c = comms_for(nshard);
   {
@@ -194,13 +195,84 @@ std::pair<double, int64_t> run_multi_gpu_sum(const HostTable &host, const std::s
     throw_on(wx_check(&L, err, sizeof(err)), err);
     if (i == 0) hip_ok(hipMemcpy(res, outs[i].ptr, 16, hipMemcpyDeviceToHost), "hipMemcpy");
   }
-  for (int i = 0; i < nshard; ++i) {
-    DevGuard g(shards[i].device);
-    keep[i] = Shard();
-  }
   int64_t cnt;
   std::memcpy(&cnt, &res[1], 8);
   return {res[0], cnt};
+}
+
+}  // namespace
+
+std::pair<double, int64_t> run_multi_gpu_sum(const HostTable &host, const std::string &expr_cuda,
+                                             const std::string &cond_cuda) {
+  auto shards = plan_shards(host.num_rows(), device_count());
+  std::vector<Shard> keep(shards.size());
+  auto r = sum_over_shards(shards, keep, expr_cuda, cond_cuda, &host);
+  for (size_t i = 0; i < keep.size(); ++i) {
+    DevGuard g(shards[i].device);
+    keep[i] = Shard();
+  }
+  return r;
+}
+
+// ------------------------------------------------------- resident shards
+struct ResidentShards::Impl {
+  int64_t n = 0;
+  std::vector<ShardRange> ranges;
+  std::vector<Shard> shards;
+  std::mutex mu;  // one query at a time per object (shared workspaces and scratch)
+};
+
+ResidentShards::ResidentShards(const HostTable &host) : impl_(new Impl) {
+  impl_->n = host.num_rows();
+  impl_->ranges = plan_shards(impl_->n, device_count());
+  impl_->shards.resize(impl_->ranges.size());
+  run_per_device(impl_->ranges, [&](size_t i, const ShardRange &r) {
+    hipStream_t s = device_stream(r.device);
+    impl_->shards[i] = upload_shard(host, r.device, r.begin, r.end, s);
+    hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize");
+  });
+}
+
+ResidentShards::~ResidentShards() {
+  for (size_t i = 0; i < impl_->shards.size(); ++i) {
+    DevGuard g(impl_->ranges[i].device);
+    impl_->shards[i] = Shard();
+  }
+}
+
+int64_t ResidentShards::num_rows() const { return impl_->n; }
+
+std::vector<float> ResidentShards::dense(const std::string &expr_cuda, const std::string &cond_cuda) const {
+  std::lock_guard<std::mutex> lk(impl_->mu);
+  std::vector<float> result = host_result(static_cast<size_t>(impl_->n));
+  run_per_device(impl_->ranges, [&](size_t i, const ShardRange &r) {
+    hipStream_t s = device_stream(r.device);
+    const int64_t rows = r.end - r.begin;
+    Scratch &scr = scratch_for(r.device);
+    std::lock_guard<std::mutex> scr_lock(scr.mu);
+    const size_t bytes = sizeof(float) * static_cast<size_t>(rows);
+    if (scr.bytes < bytes) {
+      scr.buf = DeviceBuffer();
+      scr.buf = DeviceBuffer(r.device, bytes);
+      scr.bytes = bytes;
+    }
+    float *out = static_cast<float *>(scr.buf.ptr);
+    WxTableView v(impl_->shards[i].table);
+    wx_launch L = sync_launch(r.device, s);
+    L.flags = 0;
+    char err[8192];
+    throw_on(wx_project_filter(&v.table, expr_cuda.c_str(), cond_cuda.c_str(), &L, WX_MODE_DENSE_FILL, out, nullptr,
+                               0, 0, nullptr, nullptr, err, sizeof(err)),
+             err);
+    copy_d2h(r.device, s, result.data() + r.begin, out, bytes);
+    throw_on(wx_check(&L, err, sizeof(err)), err);
+  });
+  return result;
+}
+
+std::pair<double, int64_t> ResidentShards::sum(const std::string &expr_cuda, const std::string &cond_cuda) const {
+  std::lock_guard<std::mutex> lk(impl_->mu);
+  return sum_over_shards(impl_->ranges, impl_->shards, expr_cuda, cond_cuda, nullptr);
 }
 
 }  // namespace warpdb

@@ -203,14 +203,16 @@ std::vector<float> WarpDB::query_multi_gpu(const std::string &expr) {
   if (host_table_.num_rows() == 0) throw std::runtime_error("Host table not available for multi-GPU query");
   std::string e, c;
   lower_query(expr, names_of(host_table_), e, c);
-  return run_multi_gpu_jit_host(host_table_, e, c);
+  if (!shards_) shards_ = std::make_unique<warpdb::ResidentShards>(host_table_);
+  return shards_->dense(e, c);
 }
 
 std::pair<double, int64_t> WarpDB::query_multi_gpu_sum(const std::string &expr) {
   if (host_table_.num_rows() == 0) throw std::runtime_error("Host table not available for multi-GPU query");
   std::string e, c;
   lower_query(expr, names_of(host_table_), e, c);
-  return warpdb::run_multi_gpu_sum(host_table_, e, c);
+  if (!shards_) shards_ = std::make_unique<warpdb::ResidentShards>(host_table_);
+  return shards_->sum(e, c);
 }
 
 std::vector<float> WarpDB::query_multi_gpu_csv(const std::string &csv_path, const std::string &expr,
