@@ -78,6 +78,28 @@ def test_query_dense_and_compact_vs_oracle(tmp_path):
     assert np.array_equal(np.array(chunked, np.float32).view(np.uint32), ref.view(np.uint32))
 
 
+def test_query_multi_gpu_csv_line_endings(tmp_path):
+    # the streaming chunker cuts blocks at the rows_per_chunk-th non-empty
+    # line: CRLF, blank lines and a last line without a newline must give the
+    # same rows as the whole-file loader
+    n = 30_011
+    cols = synth.c2_table(n)
+    path = tmp_path / "crlf.csv"
+    with open(path, "wb") as f:
+        f.write(b"price,quantity\r\n")
+        for i, (p, q) in enumerate(zip(cols["price"], cols["quantity"])):
+            if i % 97 == 0:
+                f.write(b"\r\n" if i % 2 else b"\n")  # blank lines
+            end = b"" if i == n - 1 else (b"\r\n" if i % 3 == 0 else b"\n")
+            f.write(f"{float(p)!r},{int(q)}".encode() + end)
+    db = pw().WarpDB(str(path))
+    whole = db.query("price * quantity WHERE price > 15")
+    assert len(whole) == n
+    for rpc in (1, 333, 30_011, 1_000_000):
+        got = pw().WarpDB.query_multi_gpu_csv(str(path), "price * quantity WHERE price > 15", rpc)
+        assert got == whole, rpc
+
+
 def test_query_errors():
     db = pw().WarpDB(TEST_CSV)
     with pytest.raises(RuntimeError, match="Unknown column: nope"):
