@@ -611,3 +611,71 @@ def test_sort_radix_large_properties():
     assert bool((t[1:] >= t[:-1]).all().item())
     b1 = t.view(torch.int32).to(torch.int64)
     assert (b1.sum().item(), (b1 * b1).sum().item()) == (s0, q0)
+
+
+# ------------------------------------------------------- concurrent streams
+def test_concurrent_streams_from_threads():
+    """Four host threads, one HIP stream each, interleave compaction, SUM, top-K
+    and radix sorts on their own tables; every result equals the serial one.
+    The runtime keeps one workspace per (device, stream) and locks only its
+    shared maps (warpexec.cpp `workspace`), so this must not race."""
+    import threading
+
+    n_threads, iters = 4, 6
+    sizes = [1_000_003, 2_500_001, 777_777, 1_300_000]
+    jobs = []
+    for t in range(n_threads):
+        n = sizes[t]
+        price = torch.empty(n, dtype=torch.float32, device="cuda")
+        qty = torch.empty(n, dtype=torch.float32, device="cuda")
+        L = launch()
+        wx.fill_synthetic(price.data_ptr(), wx.FLOAT32, n, 100 + t, 0, 0.0, 40.0, L)
+        wx.fill_synthetic(qty.data_ptr(), wx.FLOAT32, n, 200 + t, 1, 1, 100, L)
+        table = wx.Table(n, [wx.Column("price", wx.FLOAT32, price.data_ptr()),
+                             wx.Column("quantity", wx.FLOAT32, qty.data_ptr())])
+        mask = price > 15.0
+        want = {"idx": torch.nonzero(mask).flatten(), "vals": (price * qty)[mask],
+                "sorted": torch.sort(price).values}
+        s, c = wx.reduce_sum(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", L)
+        want["sum"] = (s, c)
+        k = torch.empty(5, device="cuda")
+        i = torch.empty(5, dtype=torch.int64, device="cuda")
+        v = torch.empty(5, device="cuda")
+        wx.topk(table, "price[idx]", None, "discount(price[idx], 0.9f)", 5, True, L, k.data_ptr(), i.data_ptr(),
+                v.data_ptr())
+        want["topk"] = (k.clone(), i.clone(), v.clone())
+        bufs = {"vals": torch.empty(n, device="cuda"), "idx": torch.empty(n, dtype=torch.int64, device="cuda"),
+                "sort": torch.empty(n, device="cuda"), "k": torch.empty(5, device="cuda"),
+                "i": torch.empty(5, dtype=torch.int64, device="cuda"), "v": torch.empty(5, device="cuda")}
+        jobs.append((table, price, qty, want, bufs, torch.cuda.Stream()))
+    torch.cuda.synchronize()
+    errors = []
+
+    def work(j):
+        table, price, _, want, b, stream = jobs[j]
+        try:
+            with torch.cuda.stream(stream):
+                L = wx.make_launch(device=0, stream=stream.cuda_stream, custom_src=DISCOUNT_SRC, flags=wx.F_SYNC)
+                for it in range(iters):
+                    cnt = wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", L,
+                                            wx.MODE_COMPACT, b["vals"].data_ptr(), b["idx"].data_ptr(), 8, 0,
+                                            want_count=True)
+                    assert cnt == want["idx"].numel()
+                    assert torch.equal(b["idx"][:cnt], want["idx"]) and torch.equal(b["vals"][:cnt], want["vals"])
+                    assert wx.reduce_sum(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", L) == want["sum"]
+                    wx.topk(table, "price[idx]", None, "discount(price[idx], 0.9f)", 5, True, L, b["k"].data_ptr(),
+                            b["i"].data_ptr(), b["v"].data_ptr())
+                    assert all(torch.equal(x, y) for x, y in zip((b["k"], b["i"], b["v"]), want["topk"]))
+                    b["sort"].copy_(price)
+                    wx.sort_float(b["sort"].data_ptr(), table.n_rows, True, L)
+                    assert torch.equal(b["sort"], want["sorted"]), it
+                stream.synchronize()
+        except Exception as e:  # noqa: BLE001 - reported by the main thread
+            errors.append((j, repr(e)))
+
+    th = [threading.Thread(target=work, args=(j,)) for j in range(n_threads)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errors, errors
