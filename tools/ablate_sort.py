@@ -36,6 +36,11 @@ VARIANTS = {
     "lb_first": {D: "WX_RS_LB_FIRST=1"},
     "lbw2": {"WARPDB_RS_LBW": "2"},
     "lbw2_first": {"WARPDB_RS_LBW": "2", D: "WX_RS_LB_FIRST=1"},
+    "hcopies4": {D: "WX_RS_HCOPIES=4"},
+    "hcopies16": {D: "WX_RS_HCOPIES=16"},
+    "hcopies32": {D: "WX_RS_HCOPIES=32"},
+    "hunroll2": {D: "WX_RS_HUNROLL=2"},
+    "hunroll8": {D: "WX_RS_HUNROLL=8"},
 }
 KNOBS = (D, "WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW")
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 10**9
