@@ -174,6 +174,27 @@ def test_compact_selectivity_extremes(cond):
     assert np.array_equal(bits(vals), bits(rv))
 
 
+@pytest.mark.parametrize("n,offset", [(0, 0), (5, 0), (300_001, 0), (300_001, 1)])
+def test_compact_without_where(n, offset):
+    # no WHERE and no indices: every row in order (run as the dense projection);
+    # with indices: the compaction kernel, indices 0..n-1
+    cols = synth.c2_table(n)
+    table, _ = dev_table(cols, offset=offset)
+    rv, ri = ora.project_filter(ora.HostTable(cols), "price * quantity + 1", None)
+    out = torch.full((max(1, n) + 1,), float("nan"), device="cuda")
+    vals = out[offset:offset + max(1, n)]
+    cnt = wx.project_filter(table, ora.lower("price * quantity + 1"), None, launch(), wx.MODE_COMPACT,
+                            vals.data_ptr(), 0, 8, 0, want_count=True)
+    assert cnt == n == len(rv)
+    assert np.array_equal(bits(vals[:n].cpu().numpy()), bits(rv))
+    dc = torch.full((1,), -1, dtype=torch.int64, device="cuda")
+    wx.project_filter(table, ora.lower("price * quantity + 1"), None, launch(), wx.MODE_COMPACT, 0, 0, 8, 0,
+                      d_count=dc.data_ptr())
+    assert int(dc.item()) == n
+    v2, i2 = gpu_compact(table, ora.lower("price * quantity + 1"), None)
+    assert np.array_equal(i2, ri) and np.array_equal(bits(v2), bits(rv))
+
+
 def test_compact_int32_index_and_row_base():
     n = 123_457
     cols = synth.c2_table(n, row_base=1000)
