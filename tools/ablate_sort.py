@@ -33,6 +33,7 @@ VARIANTS = {
     "items16": {"WARPDB_RS_ITEMS": "16"},
     "items24": {"WARPDB_RS_ITEMS": "24"},
     "rank_g4": {D: "WX_RS_RANK_G=4"},
+    "rank_lead0": {D: "WX_RS_RANK_LEAD=0"},
     "lb_first": {D: "WX_RS_LB_FIRST=1"},
     "lbw2": {"WARPDB_RS_LBW": "2"},
     "lbw2_first": {"WARPDB_RS_LBW": "2", D: "WX_RS_LB_FIRST=1"},

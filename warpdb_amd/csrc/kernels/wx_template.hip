@@ -1875,6 +1875,9 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_i_d(WxRadix
 #ifndef WX_RS_DIAG_NO_LOOKBACK
 #define WX_RS_DIAG_NO_LOOKBACK 0  // diagnostic: every tile takes its offset as 0 (results invalid)
 #endif
+#ifndef WX_RS_RANK_LEAD
+#define WX_RS_RANK_LEAD 1  // lane 0's digit group ranked by one ballot, without LDS
+#endif
 #ifndef WX_RS_LB_FIRST
 #define WX_RS_LB_FIRST 0  // load the first predecessor word before the in-tile scan's barrier
 #endif
@@ -1955,17 +1958,32 @@ __device__ __forceinline__ void wx_rs_rank(const WxRadixPassArgs &a, WxRsShared 
     }
 #if WX_RS_MATCH_LDS
     // the G items' ORs, then their read-backs, then their clears: one wait
-    // for the group where one item at a time waited for each
+    // for the group where one item at a time waited for each.  With
+    // WX_RS_RANK_LEAD the lanes sharing lane 0's digit take their mask from
+    // one ballot and stay off LDS: a few-valued digit (the exponent byte)
+    // would otherwise send most of the wave's ORs to one word, serialized.
+    bool lds[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      lds[g] = valid[g];
+      if (WX_RS_RANK_LEAD) {
+        const wx_u32 d0 = __builtin_amdgcn_readfirstlane(d[g]);  // lane 0 (valid if any lane is)
+        const bool lead = valid[g] && d[g] == d0;
+        m[g] = __builtin_amdgcn_ballot_w64(lead);
+        lds[g] = valid[g] && !lead;
+      }
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g)
-      if (valid[g]) atomicOr(w[g], 1ull << lane);
+      if (lds[g]) atomicOr(w[g], 1ull << lane);
 #pragma unroll
     for (int g = 0; g < G; ++g)
-      m[g] = valid[g] ? __hip_atomic_load(w[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT) : 0ull;
+      if (lds[g]) m[g] = __hip_atomic_load(w[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      else if (!valid[g]) m[g] = 0ull;
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int g = 0; g < G; ++g)
-      if (valid[g]) __hip_atomic_store(w[g], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+      if (lds[g]) __hip_atomic_store(w[g], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
 #else
 #pragma unroll
     for (int g = 0; g < G; ++g) {
