@@ -1,20 +1,31 @@
 #!/usr/bin/env python3
 """Benchmark of the WarpDB execution path on MI355X (BASELINE.json metric).
 
-Default workload (BASELINE.json `metric`, SURVEY.md 8d C2 shape at the
+Default workload (BASELINE.json `metric`, SURVEY.md 8(d) C2 shape at the
 metric's 1B rows): a synthetic 2-column float32 table (price U[0,40),
 quantity integer-valued U{1..100}) of 1e9 rows per GPU, resident in HBM,
 and the query `price * quantity WHERE price > 15` through the C ABI
-(wx_project_filter, ordered compaction: value + int32 row index per passing
-row).  One step = one query over the whole table.  With --gpus N (one process
-per GPU, torchrun) each rank owns a contiguous 1e9-row shard (weak scaling);
-the only exchange is an RCCL all-gather of the per-shard passing counts that
-places every shard's rows in the global result (src/multi_gpu_utils.cpp:5-63
-concatenates shards in device order).
+(ordered compaction: value + int32 shard-local row index per passing row).
+One step = one query over the whole table.
 
-Other workloads (--workload): sum (C4: price * 0.9 WHERE price > 20 with an
-RCCL all-reduce of the SUM), group (C3: SUM(price) GROUP BY int32 quantity,
-1K groups), topk (C5: ORDER BY price DESC LIMIT 5 with discount()).
+Every step goes through the product's row-sharded path,
+warpdb_amd.distributed.ShardedQuery, with the exchange each result needs
+(one collective per query):
+  project  all-gather of the per-shard passing counts (global placement)
+  sum      all-reduce of {sum, count} as two doubles          (C4)
+  group    all-reduce of the 4097-double key window            (C3)
+  topk     all-gather of K packed candidates + merge           (C5)
+  dense    none (WarpDB::query's dense contract, src/warpdb.cpp:243-256)
+  sort     single GPU only (ORDER BY without LIMIT: projection + radix sort)
+
+Scaling: --rows R is per GPU (weak, the default: 1e9); --total-rows T splits
+T rows over the GPUs (strong; C4 is `--workload sum --total-rows 8e9`).
+With --gpus N the driver runs one process per GPU under torchrun (RCCL).
+
+--api runs the single-process C++ path instead (pywarpdb.ResidentShards:
+one host thread and stream per device, ncclCommInitAll over devices
+0..N-1 -- WarpDB::query_multi_gpu_sum / query_multi_gpu_group), for sum and
+group; its per-step time includes the collective and the host read-back.
 
 Prints ONE JSON line (rank 0).
 """
@@ -23,6 +34,7 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import platform
 import subprocess
 import sys
 import time
@@ -34,19 +46,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 METRIC = "rows/sec + achieved HBM GB/s, 1B-row float32 project+filter, 1/2/4/8 GPU"
 DISCOUNT_SRC = "__device__ float discount(float price, float rate) {\n    return price * rate;\n}\n"
 
+# name: (query text, lowered expression, lowered condition, dominant kernel)
 WORKLOADS = {
-    # name: (query, kernel name for rocprof, read bytes/row, column spec)
-    "project": ("price * quantity WHERE price > 15", "wx_project_compact"),
-    "sum": ("SELECT SUM(price * 0.9) FROM t WHERE price > 20", "wx_reduce_sum"),
-    "group": ("SELECT SUM(price) FROM t GROUP BY quantity", "wx_group_sum"),
-    "topk": ("SELECT discount(price, 0.9) FROM t ORDER BY price DESC LIMIT 5", "wx_topk_scan"),
-    # WarpDB::query's own contract (src/warpdb.cpp:243-256): dense float[N],
-    # 0.0f where WHERE fails, written in the same pass
-    "dense": ("price * quantity WHERE price > 15", "wx_project_dense"),
-    # ORDER BY without LIMIT (query_sql): the projection, then the radix sort
-    # (jit_sort_float, src/jit.cpp:283-307); roofline over the sort's kernels
-    "sort": ("SELECT price FROM t ORDER BY price", "wx_radix_hist + wx_radix_tile_k_f_a"),
+    "project": ("price * quantity WHERE price > 15", "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)",
+                "wx_project_compact_deep"),
+    "sum": ("SELECT SUM(price * 0.9) FROM t WHERE price > 20", "(price[idx] * 0.9f)", "(price[idx] > 20.0f)",
+            "wx_reduce_sum"),
+    "group": ("SELECT SUM(price) FROM t GROUP BY quantity", "price[idx]", "quantity[idx]", "wx_group_sum"),
+    "topk": ("SELECT discount(price, 0.9) FROM t ORDER BY price DESC LIMIT 5", "price[idx]",
+             "discount(price[idx], 0.9f)", "wx_topk_scan"),
+    # WarpDB::query's own contract: dense float[N], 0.0f where WHERE fails
+    "dense": ("price * quantity WHERE price > 15", "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)",
+              "wx_project_dense"),
+    # ORDER BY without LIMIT (query_sql): the projection, then the radix
+    # sort (jit_sort_float, src/jit.cpp:283-307); roofline over the sort
+    "sort": ("SELECT price FROM t ORDER BY price", "price[idx]", None, "wx_radix_hist + wx_radix_tile_k_f_a"),
 }
+# bytes every row reads from HBM (the "HBM-read roofline" of BASELINE.md)
+READ_BYTES = {"project": 8, "dense": 8, "group": 8, "sum": 4, "topk": 4, "sort": 4}
 
 
 def parse():
@@ -54,11 +71,40 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--rows", type=float, default=1e9, help="rows per GPU")
+    p.add_argument("--rows", type=float, default=1e9, help="rows per GPU (weak scaling)")
+    p.add_argument("--total-rows", type=float, default=None, help="rows over all GPUs (strong scaling)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="project")
+    p.add_argument("--api", action="store_true", help="single-process C++ multi-GPU path (sum, group)")
     p.add_argument("--cpu-sample", type=float, default=5e7, help="rows for the CPU baseline sample")
+    p.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU run (0: all)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
+
+
+# ------------------------------------------------------------ CPU baseline
+def host_info():
+    model = platform.processor() or ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        usable = len(os.sched_getaffinity(0))
+    except AttributeError:
+        usable = os.cpu_count()
+    return {"cpu_model": model, "logical_cpus": os.cpu_count(), "usable_cpus": usable}
+
+
+def cpu_threads_default() -> int:
+    # the GPU box's share of the host (OMP_NUM_THREADS is set to it there)
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return host_info()["usable_cpus"] or 1
 
 
 def cpu_sort_baseline(sample: int):
@@ -74,22 +120,35 @@ def cpu_sort_baseline(sample: int):
     t0 = time.perf_counter()
     np.sort(v, kind="stable")
     dt = time.perf_counter() - t0
-    return {"value": round(sample / dt, 1), "unit": "rows/s", "cores": 1, "kind": "port",
+    return {"value": round(sample / dt, 1), "unit": "rows/s", "cores": 1, "kind": "port", "host": host_info(),
             "sample": f"{sample} synthetic price values, numpy stable sort (radix for float32) on one core, {dt:.2f} s"}
 
 
-def cpu_baseline(query: str, sample: int):
+def cpu_baseline(query: str, sample: int, threads: int):
     """Reference CPU evaluator on the host: oracle/_ref (the reference's own
-    eval_node, built from /root/reference) when present, else the C port."""
+    eval_node, built from /root/reference) when present, else the C port.
+    Single-threaded as the reference is; the all-cores run beside it splits
+    the rows into contiguous ranges on std::threads."""
     harness = os.path.join(ROOT, "oracle", "_ref", "ref_harness")
     if os.path.exists(harness):
-        r = subprocess.run([harness, "bench", str(sample), query], capture_output=True, text=True, timeout=900)
-        line = [l for l in r.stdout.splitlines() if l.startswith("{")]
-        if r.returncode == 0 and line:
-            d = json.loads(line[-1])
-            return {"value": round(d["rows_per_s"], 1), "unit": "rows/s", "cores": 1, "kind": "reference",
-                    "sample": f"{sample} synthetic rows (same generator), '{query}', reference eval_node "
-                              f"(src/warpdb.cpp:111-155) single thread, {d['seconds']:.2f} s"}
+        def run(t):
+            r = subprocess.run([harness, "bench", str(sample), query, str(t)], capture_output=True, text=True,
+                               timeout=900)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            return json.loads(line[-1]) if r.returncode == 0 and line else None
+
+        one = run(1)
+        if one:
+            out = {"value": round(one["rows_per_s"], 1), "unit": "rows/s", "cores": 1, "kind": "reference",
+                   "host": host_info(),
+                   "sample": f"{sample} synthetic rows (same generator), '{query}', reference eval_node "
+                             f"(src/warpdb.cpp:111-155) single thread, {one['seconds']:.2f} s"}
+            if threads > 1:
+                mt = run(threads)
+                if mt:
+                    out["all_cores"] = {"value": round(mt["rows_per_s"], 1), "unit": "rows/s", "cores": threads,
+                                        "seconds": round(mt["seconds"], 3)}
+            return out
     import numpy as np
 
     sys.path.insert(0, os.path.join(ROOT, "tests"))
@@ -102,17 +161,77 @@ def cpu_baseline(query: str, sample: int):
     oracle_lib.scan_baseline(t, query)
     dt = time.perf_counter() - t0
     del np
-    return {"value": round(sample / dt, 1), "unit": "rows/s", "cores": 1, "kind": "port",
+    return {"value": round(sample / dt, 1), "unit": "rows/s", "cores": 1, "kind": "port", "host": host_info(),
             "sample": f"{sample} synthetic rows, '{query}', oracle/warpdb_oracle.c per-row interpreter "
                       f"single thread, {dt:.2f} s"}
 
 
-def main():
-    args = parse()
+def cpu_leg(args, workload):
+    if args.no_cpu_baseline:
+        return None
+    q = {"project": "price * quantity WHERE price > 15", "dense": "price * quantity WHERE price > 15",
+         "sum": "price * 0.9 WHERE price > 20", "group": "price", "topk": "price"}.get(workload)
+    if workload == "sort":
+        return cpu_sort_baseline(int(args.cpu_sample))
+    return cpu_baseline(q, int(args.cpu_sample), args.cpu_threads or cpu_threads_default())
+
+
+# ------------------------------------------------------------------ helpers
+def columns_for(workload):
+    """(name, dtype, seed, kind, lo, hi) of the columns a workload reads."""
+    from warpdb_amd import _warpexec as wx
+
+    price = ("price", wx.FLOAT32, 1, 0, 0.0, 40.0)
+    if workload in ("sum", "topk", "sort"):
+        return [price]
+    if workload == "group":
+        return [price, ("quantity", wx.INT32, 3, 1, 0, 1023)]  # 1K int32 groups
+    return [price, ("quantity", wx.FLOAT32, 2, 1, 1, 100)]
+
+
+def line_common(args, world, n_total, elapsed, workload):
+    return {
+        "metric": METRIC if workload == "project" else f"rows/sec, {workload} ({WORKLOADS[workload][0]})",
+        "value": round(n_total * args.steps / elapsed, 1),
+        "unit": "rows/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+        "higher_is_better": True,
+        "scaling": "strong" if args.total_rows else "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic (seeded splitmix64 generator, generated in HBM)",
+    }
+
+
+def roofline(bytes_per_launch, kern_ms, read_bytes, kname, traffic, timing):
+    achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
+            "kernel_ms": round(kern_ms, 4), "bytes_per_launch": int(bytes_per_launch), "timing": timing,
+            # BASELINE.md's "HBM-read roofline": input bytes only over the same time
+            "read_only_frac": round(read_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+
+
+def pmc_traffic(workload, n):
+    pmc = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if os.path.exists(pmc):
+        with open(pmc) as f:
+            d = json.load(f)
+        if d.get("rows"):
+            return round(d["hbm_bytes_per_launch"] * n / d["rows"])
+    return None
+
+
+# ------------------------------------------------- one process per GPU
+def main_ranks(args):
     import torch
     import torch.distributed as dist
 
     from warpdb_amd import _warpexec as wx
+    from warpdb_amd import distributed as wd
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -121,7 +240,7 @@ def main():
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
     # RCCL over xGMI, one GPU per rank.  WARPDB_DIST_BACKEND=gloo lets several
     # ranks share one GPU (rehearsal of the multi-rank path on a 1-GPU box);
-    # its exchanges go through host tensors.
+    # its exchanges stage through host tensors.
     backend = os.environ.get("WARPDB_DIST_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
@@ -130,196 +249,165 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    workload = args.workload
+    if workload == "sort" and world > 1:
+        raise SystemExit("--workload sort runs on one GPU (no distributed sort on the path)")
 
-    def all_gather(out, inp):
-        if backend == "gloo":
-            parts = [torch.empty_like(inp, device="cpu") for _ in range(world)]
-            dist.all_gather(parts, inp.cpu())
-            out.copy_(torch.cat(parts))
-        else:
-            dist.all_gather_into_tensor(out, inp)
-
-    def all_reduce(t, op=dist.ReduceOp.SUM):
-        if backend == "gloo":
-            h = t.cpu()
-            dist.all_reduce(h, op=op)
-            t.copy_(h)
-        else:
-            dist.all_reduce(t, op=op)
-
-    def barrier():
-        if world > 1:
-            dist.barrier()
-
-    n = int(args.rows)
-    row_base = rank * n
+    n_total = int(args.total_rows) if args.total_rows else int(args.rows) * world
+    b, e = wd.shard_range(n_total, world, rank)
+    n = e - b
     stream = torch.cuda.current_stream().cuda_stream
     L = wx.make_launch(device=local, stream=stream, custom_src=DISCOUNT_SRC)
-    Lt = wx.make_launch(device=local, stream=stream, custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
-
-    price = torch.empty(n, dtype=torch.float32, device="cuda")
-    wx.fill_synthetic(price.data_ptr(), wx.FLOAT32, n, 1, 0, 0.0, 40.0, L, row_base=row_base)
-    if args.workload == "group":
-        qty = torch.empty(n, dtype=torch.int32, device="cuda")
-        wx.fill_synthetic(qty.data_ptr(), wx.INT32, n, 3, 1, 0, 1023, L, row_base=row_base)
-        qdt = wx.INT32
-    else:
-        qty = torch.empty(n, dtype=torch.float32, device="cuda")
-        wx.fill_synthetic(qty.data_ptr(), wx.FLOAT32, n, 2, 1, 1, 100, L, row_base=row_base)
-        qdt = wx.FLOAT32
-    table = wx.Table(n, [wx.Column("price", wx.FLOAT32, price.data_ptr()), wx.Column("quantity", qdt, qty.data_ptr())])
-    query, kname = WORKLOADS[args.workload]
-    if args.workload == "project" and os.environ.get("WARPDB_COMPACT_SCHED", "deep") == "deep":
-        kname = "wx_project_compact_deep"
+    cols = {}
+    dmap = {wx.FLOAT32: torch.float32, wx.INT32: torch.int32}
+    for name, dt, seed, kind, lo, hi in columns_for(workload):
+        t = torch.empty(max(1, n), dtype=dmap[dt], device="cuda")[:n]
+        wx.fill_synthetic(t.data_ptr(), dt, n, seed, kind, lo, hi, L, row_base=b)
+        cols[name] = t
+    sq = wd.ShardedQuery(wd.Shard(cols, b, n), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
+    query, expr, aux, kname = WORKLOADS[workload]
+    if workload == "project" and os.environ.get("WARPDB_COMPACT_SCHED", "deep") != "deep":
+        kname = "wx_project_compact"
     counts = torch.zeros(1, dtype=torch.int64, device="cuda")
-    gathered = torch.zeros(world, dtype=torch.int64, device="cuda")
 
-    if args.workload == "project":
-        out_v = torch.empty(n, dtype=torch.float32, device="cuda")
-        out_i = torch.empty(n, dtype=torch.int32, device="cuda")
+    if workload == "project":
+        out_v = torch.empty(max(1, n), dtype=torch.float32, device="cuda")
+        out_i = torch.empty(max(1, n), dtype=torch.int32, device="cuda")
 
-        def step(Lx):
-            wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", Lx, wx.MODE_COMPACT,
-                              out_v.data_ptr(), out_i.data_ptr(), 4, 0, d_count=counts.data_ptr())
-            if world > 1:  # global placement of each shard's rows
-                all_gather(gathered, counts)
-    elif args.workload == "dense":
-        out_v = torch.empty(n, dtype=torch.float32, device="cuda")
+        def step():
+            sq.compact_device(expr, aux, out_v, out_i, 4, counts)
+    elif workload == "dense":
+        out_v = torch.empty(max(1, n), dtype=torch.float32, device="cuda")
 
-        def step(Lx):
-            wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", Lx, wx.MODE_DENSE_FILL,
-                              out_v.data_ptr(), 0, 4, 0)
-    elif args.workload == "sort":
-        out_v = torch.empty(n, dtype=torch.float32, device="cuda")
+        def step():
+            wx.project_filter(sq.table, expr, aux, sq.launch, wx.MODE_DENSE_FILL, out_v.data_ptr(), 0, 4, 0)
+    elif workload == "sort":
+        out_v = torch.empty(max(1, n), dtype=torch.float32, device="cuda")
 
-        def step(Lx):
-            wx.project_filter(table, "price[idx]", None, L, wx.MODE_COMPACT, out_v.data_ptr(), 0, 4, 0,
+        def step():
+            wx.project_filter(sq.table, expr, None, sq.launch_aux, wx.MODE_COMPACT, out_v.data_ptr(), 0, 4, 0,
                               d_count=counts.data_ptr())
-            wx.sort_float(out_v.data_ptr(), n, True, Lx)  # synchronous, as jit_sort_float
-    elif args.workload == "sum":
+            wx.sort_float(out_v.data_ptr(), n, True, sq.launch)  # synchronous, as jit_sort_float
+    elif workload == "sum":
         res = torch.zeros(2, dtype=torch.float64, device="cuda")
 
-        def step(Lx):
-            wx.reduce_sum(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", Lx, d_out=res.data_ptr(),
-                          want_host=False)
-            if world > 1:
-                all_reduce(res[:1])
-    elif args.workload == "group":
-        cap = 4096
-        keys = torch.empty(cap, dtype=torch.int32, device="cuda")
-        sums = torch.empty(cap, dtype=torch.float64, device="cuda")
-        cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
-        ng = torch.zeros(1, dtype=torch.int64, device="cuda")
-
-        def step(Lx):
-            wx.group_sum(table, "price[idx]", "quantity[idx]", None, Lx, 0, cap, keys.data_ptr(), sums.data_ptr(),
-                         cnts.data_ptr(), d_n_groups=ng.data_ptr(), want_count=False)
-            if world > 1:  # dense 1K-bin partials: keys are identical on every shard
-                all_reduce(sums[:1024])
+        def step():
+            sq.sum_device(expr, aux, res)
+    elif workload == "group":
+        def step():
+            sq.group_sum_device(expr, aux, None, 0, 4096)
     else:
-        tk = torch.empty(5, dtype=torch.float32, device="cuda")
-        ti = torch.empty(5, dtype=torch.int64, device="cuda")
-        tv = torch.empty(5, dtype=torch.float32, device="cuda")
-        allk = torch.empty(world * 5, dtype=torch.float32, device="cuda")
-
-        def step(Lx):
-            wx.topk(table, "price[idx]", None, "discount(price[idx], 0.9f)", 5, True, Lx, tk.data_ptr(),
-                    ti.data_ptr(), tv.data_ptr(), row_base=row_base, d_count=counts.data_ptr(), want_count=False)
-            if world > 1:
-                all_gather(allk, tk)
+        def step():
+            sq.topk(expr, None, aux, 5, True)
 
     for _ in range(args.warmup):
-        step(L)
+        step()
     wx.check(L)
-    wx.timing_read()  # discard
-    barrier()
+    wx.timing_read()  # discard the warm-up launches
+    if world > 1:
+        dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step(Lt)
+        step()
     torch.cuda.synchronize()
-    barrier()
-    t1 = time.perf_counter()
-    elapsed = t1 - t0
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
     kern_ms, launches = wx.timing_read()
     wx.check(L)
+    kern_avg_ms = kern_ms / max(1, launches)
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
-        all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = t.item()
-        km = torch.tensor([kern_ms / max(1, launches)], dtype=torch.float64, device="cuda")
-        all_reduce(km, op=dist.ReduceOp.MAX)
-        kern_avg_ms = km.item()
-    else:
-        kern_avg_ms = kern_ms / max(1, launches)
-    if args.workload == "sort":  # the sort's kernels as one unit: per step, not per launch
-        kern_avg_ms *= launches / max(1, args.steps)
+        t = torch.tensor([elapsed, kern_avg_ms], dtype=torch.float64, device="cuda")
+        wd.all_reduce_(t, op=dist.ReduceOp.MAX)
+        elapsed, kern_avg_ms = float(t[0]), float(t[1])
 
-    # algorithmic bytes per launch of the dominant kernel (DESIGN.md)
-    passing = int(counts.item()) if args.workload in ("project",) else None
-    if args.workload == "project":
-        bytes_per_launch = n * 8 + passing * 8
-    elif args.workload in ("sum", "topk"):
-        bytes_per_launch = n * 4
-    elif args.workload == "dense":
+    # algorithmic bytes per launch of the dominant kernel (DESIGN.md 5)
+    passing = int(counts.item()) if workload == "project" else None
+    rb = READ_BYTES[workload]
+    if workload == "project":
+        bytes_per_launch = n * 8 + passing * 8  # 4 B value + 4 B int32 index per passing row
+    elif workload == "dense":
         bytes_per_launch = n * 12
-    elif args.workload == "sort":  # histogram read + 4 passes of read + write
-        bytes_per_launch = n * (4 + 4 * 8)
+    elif workload == "sort":  # histogram read + the tile passes that ran (read + write 4 B each)
+        passes = max(0, round(launches / max(1, args.steps)) - 1)
+        kern_avg_ms *= launches / max(1, args.steps)  # the sort's kernels as one unit: per step
+        bytes_per_launch = n * (4 + 8 * passes)
+        rb = 4 + 4 * passes
     else:
-        bytes_per_launch = n * 8
-    achieved = bytes_per_launch / (kern_avg_ms * 1e-3) / 1e9
-    read_bytes = n * (4 if args.workload in ("sum", "topk") else 8)
-    if args.workload == "sort":
-        read_bytes = n * (4 + 4 * 4)
-
-    total_rows = n * world * args.steps
-    value = total_rows / elapsed
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{args.workload}.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            d = json.load(f)
-        if d.get("rows"):
-            traffic = round(d["hbm_bytes_per_launch"] * n / d["rows"])
-
-    cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        q = "price * quantity WHERE price > 15" if args.workload in ("project", "dense") else {
-            "sum": "price * 0.9 WHERE price > 20", "group": "price", "topk": "price", "sort": "price"}[args.workload]
-        cpu = cpu_sort_baseline(int(args.cpu_sample)) if args.workload == "sort" else cpu_baseline(q, int(args.cpu_sample))
-
+        bytes_per_launch = n * rb
     if rank == 0:
-        line = {
-            "metric": METRIC if args.workload == "project" else f"rows/sec, 1B-row {args.workload}",
-            "value": round(value, 1),
-            "unit": "rows/s",
-            "n_gpus": world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            "higher_is_better": True,
-            "scaling": "weak",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "data": "synthetic (seeded splitmix64 generator, generated in HBM)",
-            "config": {"workload": f"{query} ({args.workload})", "rows_per_gpu": n, "total_rows": n * world,
-                       "columns": "price f32, quantity " + ("i32" if qdt == wx.INT32 else "f32"),
-                       "index": "int32 shard-local row index" if args.workload == "project" else None,
-                       "parallelism": f"row-sharded x{world}"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                         "kernel": kname, "kernel_ms": round(kern_avg_ms, 4),
-                         "bytes_per_launch": bytes_per_launch,
-                         # BASELINE.md's "HBM-read roofline": input bytes only (8 B/row for
-                         # project / group, 4 B/row for sum / top-K) over the same time
-                         "read_only_frac": round(read_bytes / (kern_avg_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)},
-            "cpu_baseline": cpu,
-        }
+        line = line_common(args, world, n_total, elapsed, workload)
+        line["config"] = {"workload": f"{query} ({workload})", "rows_per_gpu": n, "total_rows": n_total,
+                          "columns": ", ".join(f"{c} {'i32' if t.dtype == torch.int32 else 'f32'}"
+                                               for c, t in cols.items()),
+                          "index": "int32 shard-local row index" if workload == "project" else None,
+                          "exchange": {"project": "all-gather int64 counts", "sum": "all-reduce 2 x f64",
+                                       "group": "all-reduce 4097 x f64 key window", "topk": "all-gather 11 x i64",
+                                       "dense": "none", "sort": "none"}[workload] if world > 1 else "none (1 GPU)",
+                          "parallelism": f"row-sharded x{world}, one process per GPU"}
         if passing is not None:
             line["config"]["passing_rows_per_gpu"] = passing
+        line["roofline"] = roofline(bytes_per_launch, kern_avg_ms, n * rb, kname, pmc_traffic(workload, n),
+                                    "HIP events around the dominant kernel on its stream (max over ranks)")
+        line["cpu_baseline"] = cpu_leg(args, workload) if world == 1 else None
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+# ------------------------------------------- single process, C++ multi-GPU
+def main_api(args):
+    from warpdb_amd import _warpexec as wx
+    from warpdb_amd import pywarpdb as pw
+
+    workload = args.workload
+    if workload not in ("sum", "group"):
+        raise SystemExit("--api covers the C++ multi-GPU aggregates: --workload sum | group")
+    if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+        raise SystemExit("--api is one process driving every GPU; do not launch it under torchrun")
+    devs = args.gpus
+    n_total = int(args.total_rows) if args.total_rows else int(args.rows) * devs
+    dmap = {wx.FLOAT32: pw.DataType.Float32, wx.INT32: pw.DataType.Int32}
+    cols = [(nm, dmap[dt], seed, kind, lo, hi) for nm, dt, seed, kind, lo, hi in columns_for(workload)]
+    shards = pw.ResidentShards.synthetic(n_total, cols, devs)
+    query, expr, aux, kname = WORKLOADS[workload]
+
+    if workload == "sum":
+        def step():
+            return shards.sum(expr, aux)
+    else:
+        def step():
+            return shards.group_sum(expr, aux, "", 0)
+
+    for _ in range(args.warmup):
+        step()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    elapsed = time.perf_counter() - t0
+    n_max = max(e - b for _, b, e in shards.ranges())
+    line = line_common(args, shards.num_shards, n_total, elapsed, workload)
+    line["config"] = {"workload": f"{query} ({workload})", "rows_per_gpu": n_max, "total_rows": n_total,
+                      "api": "pywarpdb.ResidentShards (WarpDB::query_multi_gpu_sum / query_multi_gpu_group)",
+                      "exchange": "ncclAllReduce " + ("2 x f64" if workload == "sum" else "4097 x f64") +
+                                  " over ncclCommInitAll(devices 0..n-1)",
+                      "parallelism": f"row-sharded x{shards.num_shards}, one process, one thread + stream per GPU"}
+    # the C++ path has no per-kernel events: the whole step bounds the kernel
+    ms = elapsed / args.steps * 1e3
+    rb = READ_BYTES[workload]
+    line["roofline"] = roofline(n_max * rb, ms, n_max * rb, kname, pmc_traffic(workload, n_max),
+                                "whole step (kernel + all-reduce + host read-back): a lower bound on the kernel")
+    line["cpu_baseline"] = cpu_leg(args, workload) if shards.num_shards == 1 else None
+    print(json.dumps(line), flush=True)
+
+
+def main():
+    args = parse()
+    if args.api:
+        main_api(args)
+    else:
+        main_ranks(args)
 
 
 if __name__ == "__main__":

@@ -17,9 +17,11 @@ void jit_compile_and_launch(const std::string &expr_code, const std::string &con
 // GROUP BY SUM over N rows of (price, quantity).  Groups come out in
 // ascending key order (the reference emits first-seen order from a serial
 // scan; its tests expect std::map order).  *d_count receives the group count.
+// Sums accumulate in double and are rounded to float on the device; the
+// double scratch holds O(groups), cached per device.
 void jit_group_sum(const std::string &val_expr_code, const std::string &key_expr_code, float *d_price,
                    int *d_quantity, float *d_out_vals, int *d_out_keys, int *d_count, int N, int device_id = 0);
 
-// In-place stable sorts (bitonic on the device).
+// In-place stable sorts (LSD radix sort on the device; NaN last, -0.0 == +0.0).
 void jit_sort_pairs(int *d_keys, float *d_vals, int count, bool ascending, int device_id = 0);
 void jit_sort_float(float *d_vals, int count, bool ascending, int device_id = 0);

@@ -30,23 +30,54 @@ std::vector<ShardRange> plan_shards(int64_t n_rows, int devices);
 std::pair<double, int64_t> run_multi_gpu_sum(const HostTable &host, const std::string &expr_cuda,
                                              const std::string &cond_cuda);
 
+// Result of a GROUP BY over shards: ascending keys, double sums, counts.
+struct GroupResult {
+  std::vector<int32_t> keys;
+  std::vector<double> sums;
+  std::vector<int64_t> counts;
+};
+
+// One synthetic column (wx_fill_synthetic's counter-based generator, so each
+// device generates its own rows at their global row numbers).
+struct SyntheticColumn {
+  std::string name;
+  DataType type;
+  uint64_t seed;
+  int kind;  // 0 uniform float in [lo, hi), 1 uniform int in [lo, hi]
+  double lo, hi;
+};
+
 // The same shards kept resident in HBM across queries (uploaded once, all
 // devices concurrently): WarpDB::query_multi_gpu / query_multi_gpu_sum pay
 // the host -> HBM copy on their first call only.  The reference re-uploads
-// the whole table on every call (src/multi_gpu_utils.cpp:34-48).
+// the whole table on every call (src/multi_gpu_utils.cpp:34-48).  Shards
+// sit on devices 0..n-1 in row order (ceil(N / n) rows each).
 class ResidentShards {
  public:
-  explicit ResidentShards(const HostTable &host);
+  // the host table split over `devices` GPUs (0 = every visible one)
+  explicit ResidentShards(const HostTable &host, int devices = 0);
+  // one shard over a table already in HBM (no copy; `table` must outlive this)
+  static std::unique_ptr<ResidentShards> borrow(const Table &table);
+  // n_rows generated directly in HBM across `devices` GPUs (0 = all)
+  static std::unique_ptr<ResidentShards> synthetic(int64_t n_rows, const std::vector<SyntheticColumn> &cols,
+                                                   int devices = 0);
   ~ResidentShards();
   ResidentShards(const ResidentShards &) = delete;
   ResidentShards &operator=(const ResidentShards &) = delete;
   int64_t num_rows() const;
+  int num_shards() const;
+  std::vector<ShardRange> ranges() const;
   // dense result of num_rows() floats in row order, 0.0f where cond fails
   std::vector<float> dense(const std::string &expr_cuda, const std::string &cond_cuda) const;
-  // SUM((float)expr) WHERE cond and the passing row count (RCCL all-reduce)
+  // SUM((float)expr) WHERE cond and the passing row count (one RCCL all-reduce)
   std::pair<double, int64_t> sum(const std::string &expr_cuda, const std::string &cond_cuda) const;
+  // SUM((float)val) GROUP BY (int)key WHERE cond: keys in [key_lo, key_lo + 2048)
+  // combine through one RCCL all-reduce of the dense window, others by a host merge
+  GroupResult group_sum(const std::string &val_cuda, const std::string &key_cuda, const std::string &cond_cuda,
+                        int32_t key_lo = 0) const;
 
  private:
+  ResidentShards();
   struct Impl;
   std::unique_ptr<Impl> impl_;
 };

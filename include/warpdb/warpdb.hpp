@@ -11,10 +11,7 @@
 #include "expression.hpp"
 #include "jit.hpp"
 #include "json_loader.hpp"
-
-namespace warpdb {
-class ResidentShards;
-}
+#include "multi_gpu_utils.hpp"
 
 class WarpDB {
  public:
@@ -51,6 +48,11 @@ class WarpDB {
   std::pair<double, int64_t> query_sum(const std::string &expr);
   // SUM(expr) WHERE cond over every GPU with an RCCL all-reduce.
   std::pair<double, int64_t> query_multi_gpu_sum(const std::string &expr);
+  // "SELECT SUM(v) FROM t [WHERE c] GROUP BY k" over every GPU: per-GPU dense
+  // key-window partials combined by one RCCL all-reduce (keys outside
+  // [key_window_lo, key_window_lo + 2048) merged on the host).  Groups in
+  // ascending key order with double sums and counts (SUM / COUNT / AVG).
+  warpdb::GroupResult query_multi_gpu_group(const std::string &sql, int32_t key_window_lo = 0);
   // Zero-copy result: dense device buffer as an ArrowDeviceArray (ROCm).
   void query_arrow_device(const std::string &expr, ArrowDeviceArray *out_array, ArrowSchema *out_schema);
 
@@ -59,6 +61,7 @@ class WarpDB {
 
  private:
   void lower(const std::string &query, std::string &expr_c, std::string &cond_c) const;
+  warpdb::ResidentShards &shards();
   Table table_;
   HostTable host_table_;
   std::unique_ptr<warpdb::ResidentShards> shards_;  // query_multi_gpu*: built on first use

@@ -24,6 +24,12 @@
  *                       src/optimizer.cpp:13-17)
  *   wx_group_agg        jit_group_sum + the per-group MIN / MAX of query_sql's
  *                       AggData (src/warpdb.cpp:375-385)
+ *   wx_group_partials,  GROUP BY over row shards: per-shard
+ *   wx_group_combine    partials in an all-reduce layout and the final merge;
+ *                       the reference's multi-GPU path gathers dense results
+ *                       on the host instead (src/multi_gpu_utils.cpp:5-63)
+ *   wx_cast             device-side type conversion (jit_group_sum's float
+ *                       outputs, include/jit.hpp:15-18)
  *
  * Expression inputs are the reference's lowered C expressions over
  * identifiers `<column>[idx]` (include/expression.hpp:32-78), e.g.
@@ -92,6 +98,8 @@ typedef struct wx_launch {
 #define WX_F_SYNC 1u      /* synchronise the stream and check device errors before returning */
 #define WX_F_NO_CUSTOM 2u /* do not prepend custom.cu */
 #define WX_F_TIME 4u      /* record HIP events around the main kernel (wx_timing_read) */
+#define WX_F_F64_COUNTS 8u /* wx_reduce_sum: d_out's count is written as a double (exact below
+                            * 2^53), so ONE all-reduce of two doubles combines shards */
 
 /* wx_project_filter modes */
 #define WX_MODE_DENSE 0      /* out_vals[row] = expr where cond holds, other rows untouched (src/jit.cpp:55-61) */
@@ -139,6 +147,45 @@ wx_status wx_group_sum(const wx_table *table, const char *val_expr, const char *
                        const char *cond, const wx_launch *launch, int32_t key_window_lo,
                        int64_t capacity, int32_t *d_keys, double *d_sums, int64_t *d_counts,
                        int64_t *d_n_groups, int64_t *h_n_groups, char *err, size_t errlen);
+
+/* On WX_ERR_CAPACITY from wx_group_sum / wx_group_agg, *h_n_groups (when
+ * given) holds the number of groups found, a lower bound of the capacity
+ * needed (exact unless the general-key table itself overflowed). */
+
+/* Row-sharded GROUP BY, step 1 (per shard): SUM((float)val_expr) GROUP BY
+ * (int)key_expr WHERE cond in the exchange layout.  d_window (device,
+ * WX_GROUP_EXCHANGE_DOUBLES doubles) receives the dense key window
+ * [key_window_lo, key_window_lo + WX_GROUP_WINDOW_BINS): the sums at
+ * [0, W), the counts as doubles at [W, 2W) (exact below 2^53), and at [2W]
+ * the number of groups outside the window.  Summing the shards' buffers
+ * element-wise -- one ncclAllReduce(SUM, ncclFloat64) -- yields the global
+ * window.  Groups outside the window go to d_keys / d_sums / d_counts
+ * (ascending keys, `capacity` entries) and their count to d_n_extra /
+ * h_n_extra. */
+#define WX_GROUP_WINDOW_BINS 2048
+#define WX_GROUP_EXCHANGE_DOUBLES (2 * WX_GROUP_WINDOW_BINS + 1)
+wx_status wx_group_partials(const wx_table *table, const char *val_expr, const char *key_expr,
+                            const char *cond, const wx_launch *launch, int32_t key_window_lo,
+                            double *d_window, int64_t capacity, int32_t *d_keys, double *d_sums,
+                            int64_t *d_counts, int64_t *d_n_extra, int64_t *h_n_extra, char *err,
+                            size_t errlen);
+
+/* Row-sharded GROUP BY, step 2: the final groups in ascending key order from
+ * a combined window (wx_group_partials layout) and the combined
+ * out-of-window groups (n_extra entries, ascending keys, none inside the
+ * window; device arrays, nullable when n_extra is 0).  Writes at most
+ * `capacity` groups; the total goes to d_n_groups / h_n_groups (a host
+ * request that exceeds capacity returns WX_ERR_CAPACITY). */
+wx_status wx_group_combine(const double *d_window, int32_t key_window_lo, const int32_t *d_x_keys,
+                           const double *d_x_sums, const int64_t *d_x_counts, int64_t n_extra,
+                           const wx_launch *launch, int64_t capacity, int32_t *d_keys, double *d_sums,
+                           int64_t *d_counts, int64_t *d_n_groups, int64_t *h_n_groups, char *err,
+                           size_t errlen);
+
+/* dst[i] = (dst type) src[i] for i < n, types in wx_dtype numbering (not
+ * WX_STRING); C conversion semantics. */
+wx_status wx_cast(const void *d_src, int32_t src_dtype, void *d_dst, int32_t dst_dtype, int64_t n,
+                  const wx_launch *launch, char *err, size_t errlen);
 
 /* wx_group_sum plus per-group MIN / MAX of (float)val_expr (d_mins / d_maxs,
  * nullable, `capacity` entries; NaN skipped as in wx_reduce_stats). */

@@ -14,9 +14,32 @@
 //   ref_harness lower  "<expr>"                -> lowered CUDA-C string
 //   ref_harness tokens "<expr>"                -> one token per line
 //   ref_harness eval   <csv> "<query>" [schema] -> "idx hexfloat" per passing row
-//   ref_harness bench  <rows> "<query>"        -> JSON timing of the reference
+//   ref_harness bench  <rows> "<query>" [threads]
+//                                              -> JSON timing of the reference
 //                                                 evaluator over synthetic rows
+//                                                 (threads > 1: contiguous row
+//                                                 ranges on std::threads, the
+//                                                 per-range row lists joined in
+//                                                 order; the reference itself is
+//                                                 single-threaded)
+//   ref_harness groupsum <csv> "<val>" "<key>" [schema]
+//                                              -> "key hexdouble count" per group:
+//                                                 the reference query_sql's CPU
+//                                                 aggregation (std::map<int,
+//                                                 AggData>, double sums,
+//                                                 src/warpdb.cpp:375-385) over
+//                                                 the reference's eval_node
+//   ref_harness topk <csv> "<order>" k desc [schema]
+//                                              -> "row hexfloat" of the first k
+//                                                 rows of a stable sort by the
+//                                                 reference's eval_node value
+//                                                 (the intent of ORDER BY .. LIMIT,
+//                                                 tests/sql_features_test.cpp:24-30)
+#include <algorithm>
 #include <chrono>
+#include <cmath>
+#include <map>
+#include <thread>
 #include <cstdint>
 #include <cstdio>
 #include <cstring>
@@ -129,6 +152,7 @@ int main(int argc, char **argv) {
       auto ex = parse_expression(tokenize(e));
       std::unique_ptr<ASTNode> cx;
       if (!c.empty()) cx = parse_expression(tokenize(c));
+      const int threads = argc >= 5 ? std::max(1, std::atoi(argv[4])) : 1;
       std::vector<float> out;
       std::vector<int> rows;
       out.reserve(n);
@@ -136,17 +160,75 @@ int main(int argc, char **argv) {
       auto t0 = std::chrono::steady_clock::now();
       // The reference CPU path: ascending row list of passing rows
       // (src/warpdb.cpp:336-344) then eval_node per row (:457-459).
-      for (int i = 0; i < static_cast<int>(n); ++i) {
-        if (cx && !eval_condition(cx.get(), h, i)) continue;
-        rows.push_back(i);
-        out.push_back(eval_node(ex.get(), h, i));
+      auto scan = [&](int b, int e, std::vector<int> &rw, std::vector<float> &ov) {
+        for (int i = b; i < e; ++i) {
+          if (cx && !eval_condition(cx.get(), h, i)) continue;
+          rw.push_back(i);
+          ov.push_back(eval_node(ex.get(), h, i));
+        }
+      };
+      if (threads == 1) {
+        scan(0, static_cast<int>(n), rows, out);
+      } else {
+        std::vector<std::vector<int>> rw(threads);
+        std::vector<std::vector<float>> ov(threads);
+        std::vector<std::thread> th;
+        const long long chunk = (n + threads - 1) / threads;
+        for (int t = 0; t < threads; ++t)
+          th.emplace_back([&, t] {
+            const long long b = std::min(n, t * chunk), e = std::min(n, b + chunk);
+            rw[t].reserve(e - b);
+            ov[t].reserve(e - b);
+            scan(static_cast<int>(b), static_cast<int>(e), rw[t], ov[t]);
+          });
+        for (auto &x : th) x.join();
+        for (int t = 0; t < threads; ++t) {
+          rows.insert(rows.end(), rw[t].begin(), rw[t].end());
+          out.insert(out.end(), ov[t].begin(), ov[t].end());
+        }
       }
       auto t1 = std::chrono::steady_clock::now();
       double s = std::chrono::duration<double>(t1 - t0).count();
       double chk = 0;
       for (float v : out) chk += v;
-      std::printf("{\"rows\": %lld, \"seconds\": %.6f, \"rows_per_s\": %.1f, \"passing\": %zu, \"checksum\": %.6f}\n",
-                  n, s, n / s, rows.size(), chk);
+      std::printf("{\"rows\": %lld, \"threads\": %d, \"seconds\": %.6f, \"rows_per_s\": %.1f, \"passing\": %zu, "
+                  "\"checksum\": %.6f}\n",
+                  n, threads, s, n / s, rows.size(), chk);
+      return 0;
+    }
+    if (mode == "groupsum" && argc >= 5) {
+      std::vector<DataType> schema;
+      if (argc >= 6)
+        for (const char *c = argv[5]; *c; ++c) schema.push_back(static_cast<DataType>(*c - '0'));
+      HostTable h = load_csv_to_host(argv[2], schema);
+      auto val = parse_expression(tokenize(argv[3]));
+      auto key = parse_expression(tokenize(argv[4]));
+      std::map<int, std::pair<double, long long>> groups;  // AggData's sum / count
+      for (int i = 0; i < h.num_rows(); ++i) {
+        auto &g = groups[static_cast<int>(eval_node(key.get(), h, i))];
+        g.first += eval_node(val.get(), h, i);
+        g.second += 1;
+      }
+      for (auto &kv : groups) std::printf("%d %a %lld\n", kv.first, kv.second.first, kv.second.second);
+      return 0;
+    }
+    if (mode == "topk" && argc >= 6) {
+      std::vector<DataType> schema;
+      if (argc >= 7)
+        for (const char *c = argv[6]; *c; ++c) schema.push_back(static_cast<DataType>(*c - '0'));
+      HostTable h = load_csv_to_host(argv[2], schema);
+      auto ord = parse_expression(tokenize(argv[3]));
+      const int k = std::atoi(argv[4]);
+      const bool desc = std::atoi(argv[5]) != 0;
+      std::vector<std::pair<float, int>> v;
+      for (int i = 0; i < h.num_rows(); ++i) v.push_back({eval_node(ord.get(), h, i), i});
+      // NaN last in either direction, ties keep row order (a stable sort)
+      std::stable_sort(v.begin(), v.end(), [&](const std::pair<float, int> &a, const std::pair<float, int> &b) {
+        if (std::isnan(a.first) || std::isnan(b.first)) return !std::isnan(a.first) && std::isnan(b.first);
+        return desc ? a.first > b.first : a.first < b.first;
+      });
+      for (int i = 0; i < k && i < static_cast<int>(v.size()); ++i)
+        std::printf("%d %a\n", v[i].second, static_cast<double>(v[i].first));
       return 0;
     }
   } catch (const std::exception &ex) {

@@ -26,6 +26,30 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+def group_partials_emulated(keys, sums, counts, key_lo):
+    """What wx_group_partials leaves for one shard (include/warpexec.h): the
+    dense window [sums | counts as f64 | out-of-window group count] and the
+    out-of-window groups.  The device kernel itself is covered by the GPU tests."""
+    W = 2048
+    win = np.zeros(2 * W + 1, np.float64)
+    inside = (keys >= key_lo) & (keys < key_lo + W)
+    win[keys[inside] - key_lo] = sums[inside]
+    win[W + keys[inside] - key_lo] = counts[inside]
+    win[2 * W] = float((~inside).sum())
+    return win, keys[~inside].astype(np.int32), sums[~inside], counts[~inside]
+
+
+def group_combine_emulated(win, key_lo, xk, xs, xc):
+    """wx_group_combine's contract: ascending keys over window bins + extras."""
+    W = 2048
+    bins = np.nonzero(win[W:2 * W])[0]
+    keys = np.concatenate([xk.astype(np.int64), bins + key_lo])
+    sums = np.concatenate([xs, win[bins]])
+    cnts = np.concatenate([xc, win[W + bins].astype(np.int64)])
+    o = np.argsort(keys, kind="stable")
+    return keys[o].astype(np.int32), sums[o], cnts[o]
+
+
 def _worker(rank: int, world: int, port: int, n: int, errq):
     try:
         sys.path[:0] = [ROOT, HERE]
@@ -57,12 +81,32 @@ def _worker(rank: int, world: int, port: int, n: int, errq):
         rs, rc = ora.reduce_sum(ora.HostTable(full2), "price * 0.9", "price > 20")
         assert gc == rc and abs(gs - rs) <= 1e-9 * abs(rs)
 
-        # GROUP BY
+        # GROUP BY: the general merge, and the product's exchange (dense
+        # window all-reduce + merge of the out-of-window groups only).  With
+        # key_lo = 512 half of the 1024 keys fall outside the window.
         k, sm, cn = ora.group_sum(loc3, "price", "quantity")
         gk, gsum, gcnt = wd.merge_groups(torch.from_numpy(k), torch.from_numpy(sm), torch.from_numpy(cn), len(k))
         rk, rsum, rcnt = ora.group_sum(ora.HostTable(full3), "price", "quantity")
         assert np.array_equal(gk.numpy(), rk) and np.array_equal(gcnt.numpy(), rcnt)
         assert np.array_equal(gsum.numpy(), rsum)  # exact: float values summed in double
+        for key_lo in (0, 512, -5000):
+            win, xk, xs, xc = group_partials_emulated(k, sm, cn, key_lo)
+            wt = torch.from_numpy(win)
+            wd.exchange_group_window(wt)
+            n_extra_total = int(wt[2 * wd.GROUP_WINDOW_BINS].item())
+            outside = int(((rk < key_lo) | (rk >= key_lo + wd.GROUP_WINDOW_BINS)).sum())
+            assert (n_extra_total > 0) == (outside > 0) and n_extra_total >= outside  # shards' counts, summed
+            mk = np.zeros(0, np.int32); ms = np.zeros(0); mc = np.zeros(0, np.int64)
+            if n_extra_total:
+                a, b_, c_ = wd.merge_groups(torch.from_numpy(xk), torch.from_numpy(xs), torch.from_numpy(xc), len(xk))
+                mk, ms, mc = a.numpy(), b_.numpy(), c_.numpy()
+            ck, cs, cc = group_combine_emulated(wt.numpy(), key_lo, mk, ms, mc)
+            assert np.array_equal(ck, rk) and np.array_equal(cc, rcnt) and np.array_equal(cs, rsum), key_lo
+
+        # SUM through the product's one-collective layout {sum, count as f64}
+        out = torch.tensor([s, float(c)], dtype=torch.float64)
+        wd.exchange_sum_device(out)
+        assert int(out[1]) == rc and abs(float(out[0]) - rs) <= 1e-9 * abs(rs)
 
         # top-K with ties (quantised keys) in both directions
         for desc in (True, False):

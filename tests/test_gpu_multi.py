@@ -1,0 +1,299 @@
+"""GPU tests of the row-sharded (multi-GPU) path and the round-2 ABI additions.
+
+* GROUP BY exchange: wx_group_partials on several shards (views of one
+  table on cuda:0, or real devices when more than one is visible), the
+  windows summed element-wise as the all-reduce does, wx_group_combine ->
+  equal to the oracle over the whole table, keys outside the window included.
+* SUM in the one-collective layout (WX_F_F64_COUNTS), wx_cast.
+* Compaction status epochs: more than 63 launches on one workspace (epoch
+  wrap), shrinking / growing tables, every result bit-exact.
+* warpdb_amd.distributed.ShardedQuery without a process group (1 GPU) and
+  the C++ ResidentShards (synthetic shards, sum / group_sum) on every
+  visible device, against the oracle.
+* Two host threads on one WarpDB (workspace lock).
+* bench.py end to end at small sizes for every workload (JSON contract).
+"""
+from __future__ import annotations
+
+import json
+import os
+import subprocess
+import sys
+import threading
+
+import numpy as np
+import pytest
+
+import oracle_lib as ora
+import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+from warpdb_amd import _warpexec as wx  # noqa: E402
+from test_gpu_parity import dev_table, launch, bits, GOLDEN  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W = wx.GROUP_WINDOW_BINS
+
+
+def _shard_views(cols, k):
+    """k contiguous row shards of one device table (ceil(n / k) rows each)."""
+    n = len(next(iter(cols.values())))
+    table, tensors = dev_table(cols)
+    chunk = (n + k - 1) // k
+    out = []
+    for r in range(k):
+        b, e = min(n, r * chunk), min(n, (r + 1) * chunk)
+        sub = {name: t[b:e] for name, t in tensors.items()}
+        out.append((b, wx.Table.from_tensors(**sub) if e > b else None))
+    return out
+
+
+def _partials(table, val, key, cond, key_lo, cap=1 << 14):
+    win = torch.full((wx.GROUP_EXCHANGE_DOUBLES,), float("nan"), dtype=torch.float64, device="cuda")
+    xk = torch.empty(cap, dtype=torch.int32, device="cuda")
+    xs = torch.empty(cap, dtype=torch.float64, device="cuda")
+    xc = torch.empty(cap, dtype=torch.int64, device="cuda")
+    nx = wx.group_partials(table, val, key, cond, launch(), key_lo, win.data_ptr(), cap, xk.data_ptr(),
+                           xs.data_ptr(), xc.data_ptr(), want_count=True)
+    return win, xk[:nx], xs[:nx], xc[:nx]
+
+
+def _combine(win, key_lo, mk, ms, mc, cap=1 << 14):
+    ok = torch.empty(cap, dtype=torch.int32, device="cuda")
+    os_ = torch.empty(cap, dtype=torch.float64, device="cuda")
+    oc = torch.empty(cap, dtype=torch.int64, device="cuda")
+    m = mk.numel()
+    g = wx.group_combine(win.data_ptr(), key_lo, mk.data_ptr() if m else 0, ms.data_ptr() if m else 0,
+                         mc.data_ptr() if m else 0, m, launch(), cap, ok.data_ptr(), os_.data_ptr(), oc.data_ptr(),
+                         want_count=True)
+    return ok[:g].cpu().numpy(), os_[:g].cpu().numpy(), oc[:g].cpu().numpy()
+
+
+@pytest.mark.parametrize("shards", [1, 2, 3, 8])
+@pytest.mark.parametrize("key_lo", [0, 512, -100_000])
+def test_group_exchange_matches_oracle(shards, key_lo):
+    n = 300_007
+    cols = synth.c3_table(n)
+    total = torch.zeros(wx.GROUP_EXCHANGE_DOUBLES, dtype=torch.float64, device="cuda")
+    xs_all = []
+    for _, t in _shard_views(cols, shards):
+        if t is None:
+            continue
+        win, xk, xs, xc = _partials(t, "price[idx]", "quantity[idx]", "(price[idx] < 35.0f)", key_lo)
+        assert not torch.isnan(win).any()
+        assert int(win[2 * W].item()) == xk.numel()
+        total += win  # what the all-reduce computes
+        xs_all.append((xk, xs, xc))
+    k = torch.cat([a for a, _, _ in xs_all]).long()
+    s = torch.cat([b for _, b, _ in xs_all])
+    c = torch.cat([c for _, _, c in xs_all])
+    uk, inv = torch.unique(k, sorted=True, return_inverse=True)
+    ms = torch.zeros(uk.numel(), dtype=torch.float64, device="cuda").index_add_(0, inv, s)
+    mc = torch.zeros(uk.numel(), dtype=torch.int64, device="cuda").index_add_(0, inv, c)
+    gk, gs, gc = _combine(total, key_lo, uk.int().contiguous(), ms, mc)
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", "price < 35")
+    assert np.array_equal(gk, rk) and np.array_equal(gc, rc)
+    np.testing.assert_allclose(gs, rs, rtol=1e-12, atol=0)  # double sums of float values, shard order differs
+    if shards == 1:
+        assert np.array_equal(gs, rs)
+
+
+def test_group_partials_window_layout_and_clean_state():
+    cols = {"price": np.array([1.5, 2.0, 4.0, 8.0, 16.0], np.float32),
+            "k": np.array([0, 2047, 2048, -1, 0], np.int32)}
+    table, _ = dev_table(cols)
+    for _ in range(2):  # the second call finds the accumulators clean
+        win, xk, xs, xc = _partials(table, "price[idx]", "k[idx]", None, 0)
+        w = win.cpu().numpy()
+        assert w[0] == 17.5 and w[W + 0] == 2 and w[2047] == 2.0 and w[W + 2047] == 1
+        assert w[2 * W] == 2 and np.count_nonzero(w[:2 * W]) == 4
+        assert xk.cpu().tolist() == [-1, 2048] and xs.cpu().tolist() == [8.0, 4.0] and xc.cpu().tolist() == [1, 1]
+    # a plain GROUP BY afterwards is unaffected
+    keys = torch.empty(8, dtype=torch.int32, device="cuda")
+    sums = torch.empty(8, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(8, dtype=torch.int64, device="cuda")
+    g = wx.group_sum(table, "price[idx]", "k[idx]", None, launch(), 0, 8, keys.data_ptr(), sums.data_ptr(),
+                     cnts.data_ptr())
+    assert keys[:g].cpu().tolist() == [-1, 0, 2047, 2048] and sums[:g].cpu().tolist() == [8.0, 17.5, 2.0, 4.0]
+
+
+def test_group_combine_capacity_reports_total():
+    win = torch.zeros(wx.GROUP_EXCHANGE_DOUBLES, dtype=torch.float64, device="cuda")
+    win[W: W + 10] = 1.0
+    with pytest.raises(wx.WarpExecError) as e:
+        _combine(win, 0, torch.empty(0, dtype=torch.int32, device="cuda"),
+                 torch.empty(0, dtype=torch.float64, device="cuda"), torch.empty(0, dtype=torch.int64, device="cuda"),
+                 cap=4)
+    assert e.value.status == wx.WX_ERR_CAPACITY
+
+
+def test_reduce_sum_f64_count_layout():
+    cols = synth.c2_table(1_000_003)
+    table, _ = dev_table(cols)
+    out = torch.zeros(2, dtype=torch.float64, device="cuda")
+    wx.reduce_sum(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", launch(wx.F_SYNC | wx.F_F64_COUNTS),
+                  d_out=out.data_ptr(), want_host=False)
+    rs, rc = ora.reduce_sum(ora.HostTable(cols), "price * 0.9", "price > 20")
+    assert out[1].item() == float(rc) and out[0].item() == rs
+    s, c = wx.reduce_sum(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", launch(wx.F_SYNC | wx.F_F64_COUNTS),
+                         d_out=out.data_ptr())
+    assert c == rc and s == rs
+
+
+@pytest.mark.parametrize("src,dst", [(torch.float64, torch.float32), (torch.int64, torch.int32),
+                                     (torch.float32, torch.int64), (torch.int32, torch.float64)])
+def test_cast(src, dst):
+    dt = {torch.int32: wx.INT32, torch.int64: wx.INT64, torch.float32: wx.FLOAT32, torch.float64: wx.FLOAT64}
+    n = 100_003
+    a = (torch.arange(n, device="cuda", dtype=torch.float64) * 1.37 - 5e4).to(src)
+    b = torch.empty(n, dtype=dst, device="cuda")
+    wx.cast(a.data_ptr(), dt[src], b.data_ptr(), dt[dst], n, launch())
+    assert torch.equal(b, a.to(dst))
+
+
+def test_compaction_epochs_wrap_and_shrink():
+    """70 compactions on one workspace with sizes going up and down: the
+    status words are never cleared between launches (epoch tags) and the
+    ticket returns to 0 by itself; every result must be exact."""
+    big = synth.c2_table(2_000_003)
+    table_big, tens = dev_table(big)
+    rv, ri = ora.project_filter(ora.HostTable(big), "price * quantity", "price > 15")
+    sizes = [2_000_003, 12_289, 1, 1_000_000, 0, 524_288, 2_000_003]
+    vals = torch.empty(2_000_003, dtype=torch.float32, device="cuda")
+    idx = torch.empty(2_000_003, dtype=torch.int64, device="cuda")
+    for it in range(70):
+        n = sizes[it % len(sizes)]
+        sub = wx.Table.from_tensors(price=tens["price"][:n], quantity=tens["quantity"][:n]) if n else \
+            wx.Table(0, [wx.Column("price", wx.FLOAT32, 0), wx.Column("quantity", wx.FLOAT32, 0)])
+        cnt = wx.project_filter(sub, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", launch(),
+                                wx.MODE_COMPACT, vals.data_ptr(), idx.data_ptr(), 8, 0, want_count=True)
+        m = int(np.searchsorted(ri, n))
+        assert cnt == m, (it, n)
+        assert np.array_equal(idx[:cnt].cpu().numpy(), ri[:m]), (it, n)
+        assert np.array_equal(bits(vals[:cnt].cpu().numpy()), bits(rv[:m])), (it, n)
+    del table_big
+
+
+def test_sharded_query_single_process_matches_oracle():
+    from warpdb_amd import distributed as wd
+
+    n = 500_009
+    c2, c3 = synth.c2_table(n), synth.c3_table(n)
+    t2 = {k: torch.from_numpy(v).cuda() for k, v in c2.items()}
+    t3 = {k: torch.from_numpy(v).cuda() for k, v in c3.items()}
+    q2 = wd.ShardedQuery(wd.Shard(t2, 0, n), custom_src=DISCOUNT)
+    v, i, off, total = q2.compact("(price[idx] * quantity[idx])", "(price[idx] > 15.0f)")
+    rv, ri = ora.project_filter(ora.HostTable(c2), "price * quantity", "price > 15")
+    assert off == 0 and total == len(ri)
+    assert np.array_equal(i.cpu().numpy(), ri) and np.array_equal(bits(v.cpu().numpy()), bits(rv))
+    s, c = q2.sum("(price[idx] * 0.9f)", "(price[idx] > 20.0f)")
+    rs, rc = ora.reduce_sum(ora.HostTable(c2), "price * 0.9", "price > 20")
+    assert c == rc and s == rs
+    q3 = wd.ShardedQuery(wd.Shard(t3, 0, n))
+    k, sm, cn = q3.group_sum("price[idx]", "quantity[idx]", None)
+    rk, rsum, rcnt = ora.group_sum(ora.HostTable(c3), "price", "quantity")
+    assert np.array_equal(k.cpu().numpy(), rk) and np.array_equal(cn.cpu().numpy(), rcnt)
+    assert np.array_equal(sm.cpu().numpy(), rsum)
+    # keys partly outside the window: the extras path
+    k, sm, cn = q3.group_sum("price[idx]", "quantity[idx]", None, key_lo=300)
+    assert np.array_equal(k.cpu().numpy(), rk) and np.array_equal(sm.cpu().numpy(), rsum)
+    tk, ti, tv = q2.topk("price[idx]", None, "discount(price[idx], 0.9f)", 5, True)
+    ok_, oi, ov = ora.topk(ora.HostTable(c2), "price", 5, True, select_expr="discount(price, 0.9)")
+    assert np.array_equal(ti.numpy(), oi) and np.array_equal(bits(tk.numpy()), bits(ok_))
+    assert np.array_equal(bits(tv.numpy()), bits(ov))
+
+
+DISCOUNT = "__device__ float discount(float price, float rate) {\n    return price * rate;\n}\n"
+
+
+@pytest.mark.parametrize("devices", ["one", "all"])
+def test_resident_shards_synthetic_sum_and_group(devices):
+    from warpdb_amd import pywarpdb as pw
+
+    ndev = torch.cuda.device_count()
+    d = 1 if devices == "one" else ndev
+    if devices == "all" and ndev < 2:
+        pytest.skip("one GPU visible: the all-devices case runs on multi-GPU boxes")
+    n = 1_000_003
+    cols = [("price", pw.DataType.Float32, 1, 0, 0.0, 40.0), ("quantity", pw.DataType.Int32, 3, 1, 0, 1023)]
+    rs_ = pw.ResidentShards.synthetic(n, cols, d)
+    assert rs_.num_shards == d and rs_.num_rows == n
+    host = synth.c3_table(n)
+    s, c = rs_.sum("(price[idx] * 0.9f)", "(price[idx] > 20.0f)")
+    es, ec = ora.reduce_sum(ora.HostTable(host), "price * 0.9", "price > 20")
+    assert c == ec and abs(s - es) <= 1e-12 * abs(es)
+    for key_lo in (0, 700):
+        k, sm, cn = rs_.group_sum("price[idx]", "quantity[idx]", "", key_lo)
+        rk, rsum, rcnt = ora.group_sum(ora.HostTable(host), "price", "quantity")
+        assert np.array_equal(k, rk) and np.array_equal(cn, rcnt)
+        np.testing.assert_allclose(sm, rsum, rtol=1e-12, atol=0)
+
+
+def test_warpdb_multi_gpu_group_and_shared_table():
+    from warpdb_amd import pywarpdb as pw
+
+    db = pw.WarpDB(os.path.join(GOLDEN, "test.csv"))
+    k, s, c = db.query_multi_gpu_group("SELECT SUM(price) FROM test GROUP BY quantity")
+    # tests/sql_features_test.cpp:11-22: keys 2,3,4,5 -> 15.25, 10.5, 20, 30
+    assert k.tolist() == [2, 3, 4, 5] and s.tolist() == [15.25, 10.5, 20.0, 30.0] and c.tolist() == [1, 1, 1, 1]
+    k, s, c = db.query_multi_gpu_group("SELECT SUM(price) FROM test WHERE price > 12 GROUP BY quantity")
+    assert k.tolist() == [2, 4, 5] and s.tolist() == [15.25, 20.0, 30.0]
+    assert db.query_multi_gpu_sum("price * 0.9 WHERE price > 20") == pytest.approx((27.0, 1))
+    r = db.query_multi_gpu("price * quantity WHERE price > 10")
+    assert list(r) == [31.5, 80.0, 30.5, 150.0]
+
+
+def test_two_threads_share_one_warpdb():
+    """pywarpdb releases the GIL; both threads use the null stream's
+    workspace: the per-workspace lock keeps their sorts apart."""
+    from warpdb_amd import pywarpdb as pw
+
+    path = os.path.join(ROOT, "gpurun_out", "threads_table.csv")
+    os.makedirs(os.path.dirname(path), exist_ok=True)
+    n = 200_000
+    cols = synth.c2_table(n)
+    with open(path, "w") as f:
+        f.write("price,quantity\n")
+        for p, q in zip(cols["price"].tolist(), cols["quantity"].tolist()):
+            f.write("%.9g,%d\n" % (p, int(q)))
+    db = pw.WarpDB(path)
+    expect = np.sort(db.query_sql("SELECT price FROM t WHERE price > 5"))[::-1]
+    errors = []
+
+    def worker():
+        try:
+            for _ in range(6):
+                r = np.asarray(db.query_sql("SELECT price FROM t WHERE price > 5 ORDER BY price DESC"))
+                if not np.array_equal(r, expect):
+                    errors.append("wrong order")
+                g = np.asarray(db.query_sql("SELECT SUM(price) FROM t GROUP BY quantity"))
+                if len(g) != 100:
+                    errors.append("wrong group count")
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=worker) for _ in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(timeout=300)
+    assert not errors, errors
+
+
+@pytest.mark.parametrize("args", [
+    ["--workload", "project"], ["--workload", "sum", "--total-rows", "3000001"], ["--workload", "group"],
+    ["--workload", "topk"], ["--workload", "dense"], ["--workload", "sort"],
+    ["--workload", "sum", "--api", "--total-rows", "3000001"], ["--workload", "group", "--api"]])
+def test_bench_json_contract(args):
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rows", "2000003", "--steps", "3", "--warmup", "1",
+           "--no-cpu-baseline"] + args
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                "scaling", "vs_baseline", "dtype", "data", "config", "roofline", "cpu_baseline"):
+        assert key in line, key
+    assert line["value"] > 0 and line["roofline"]["achieved"] > 0 and line["roofline"]["frac"] < 1.0
+    assert line["scaling"] == ("strong" if "--total-rows" in args else "weak")

@@ -32,6 +32,10 @@ INT32, INT64, FLOAT32, FLOAT64, STRING = 0, 1, 2, 3, 4
 F_SYNC = 1
 F_NO_CUSTOM = 2
 F_TIME = 4
+F_F64_COUNTS = 8  # reduce_sum: count written as a double (one f64 all-reduce combines shards)
+
+GROUP_WINDOW_BINS = 2048
+GROUP_EXCHANGE_DOUBLES = 2 * GROUP_WINDOW_BINS + 1  # [sums | counts as f64 | out-of-window groups]
 
 MODE_DENSE = 0
 MODE_DENSE_FILL = 1
@@ -45,6 +49,9 @@ EXPORTED_SYMBOLS = (
     "wx_reduce_stats",
     "wx_group_sum",
     "wx_group_agg",
+    "wx_group_partials",
+    "wx_group_combine",
+    "wx_cast",
     "wx_topk",
     "wx_sort_pairs",
     "wx_sort_float",
@@ -116,6 +123,9 @@ def load() -> ctypes.CDLL:
         "wx_reduce_stats": [T, E, E, L, P, ctypes.POINTER(WxStats), E, S],
         "wx_group_sum": [T, E, E, E, L, I32, I64, P, P, P, P, pI64, E, S],
         "wx_group_agg": [T, E, E, E, L, I32, I64, P, P, P, P, P, P, pI64, E, S],
+        "wx_group_partials": [T, E, E, E, L, I32, P, I64, P, P, P, P, pI64, E, S],
+        "wx_group_combine": [P, I32, P, P, P, I64, L, I64, P, P, P, P, pI64, E, S],
+        "wx_cast": [P, I32, P, I32, I64, L, E, S],
         "wx_topk": [T, E, E, E, I32, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_sort_pairs": [P, P, I64, I32, L, E, S],
         "wx_sort_float": [P, I64, I32, L, E, S],
@@ -261,6 +271,43 @@ def group_agg(table: Table, val_expr: str, key_expr: str, cond: Optional[str], l
                           ctypes.byref(h) if want_count else None, err, len(err))
     _check(st, err)
     return h.value if want_count else None
+
+
+def group_partials(table: Table, val_expr: str, key_expr: str, cond: Optional[str], launch: WxLaunch,
+                   key_window_lo: int, d_window: int, capacity: int, d_keys: int, d_sums: int, d_counts: int,
+                   d_n_extra: int = 0, want_count: bool = False) -> Optional[int]:
+    """Per-shard GROUP BY partials in the exchange layout (include/warpexec.h)."""
+    lib = load()
+    err = _err()
+    h = ctypes.c_int64(-1)
+    st = lib.wx_group_partials(ctypes.byref(table.c), _enc(val_expr), _enc(key_expr), _enc(cond),
+                               ctypes.byref(launch), key_window_lo, d_window, capacity, d_keys or None,
+                               d_sums or None, d_counts or None, d_n_extra or None,
+                               ctypes.byref(h) if want_count else None, err, len(err))
+    _check(st, err)
+    return h.value if want_count else None
+
+
+def group_combine(d_window: int, key_window_lo: int, d_x_keys: int, d_x_sums: int, d_x_counts: int, n_extra: int,
+                  launch: WxLaunch, capacity: int, d_keys: int, d_sums: int, d_counts: int, d_n_groups: int = 0,
+                  want_count: bool = False) -> Optional[int]:
+    """Final groups from a combined exchange window + combined out-of-window groups."""
+    lib = load()
+    err = _err()
+    h = ctypes.c_int64(-1)
+    st = lib.wx_group_combine(d_window, key_window_lo, d_x_keys or None, d_x_sums or None, d_x_counts or None,
+                              n_extra, ctypes.byref(launch), capacity, d_keys or None, d_sums or None,
+                              d_counts or None, d_n_groups or None, ctypes.byref(h) if want_count else None,
+                              err, len(err))
+    _check(st, err)
+    return h.value if want_count else None
+
+
+def cast(d_src: int, src_dtype: int, d_dst: int, dst_dtype: int, n: int, launch: WxLaunch) -> None:
+    lib = load()
+    err = _err()
+    _check(lib.wx_cast(d_src or None, src_dtype, d_dst or None, dst_dtype, n, ctypes.byref(launch), err, len(err)),
+           err)
 
 
 def topk(table: Table, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int, descending: bool,

@@ -48,6 +48,7 @@ typedef unsigned int wx_u32;
 #endif
 #define WX_RS_TILE (WX_RS_BLOCK * WX_RS_ITEMS)
 #define WX_RS_EPOCHS 63
+#define WX_CS_EPOCHS 63  // compaction status epochs (6 bits, 0 = never written)
 
 struct WxDenseArgs {
   const void *col[WX_MAX_COLS];
@@ -60,13 +61,14 @@ struct WxCompactArgs {
   const void *col[WX_MAX_COLS];
   float *out_val;     // nullable
   void *out_idx;      // nullable; int32 or int64
-  wx_u64 *status;     // [n_tiles + 1], zeroed per call; [n_tiles] = abort word
-  wx_u64 *ctrs;       // [0] tile ticket (zeroed per call), [1] error bits
+  wx_u64 *status;     // [n_tiles + 1] {epoch:6 | flag:2 | value:56}; [n_tiles] = abort word
+  wx_u64 *ctrs;       // [0] tile ticket, [1] error bits, [2] retired workgroups (0 between launches)
   wx_i64 *count_out;  // nullable
   wx_i64 n_rows;
   wx_i64 n_tiles;
   wx_i64 row_base;
   int idx64;
+  wx_u32 epoch;  // 1..WX_CS_EPOCHS: tags this launch's status words
   wx_u64 *diag;  // nullable; WX_DIAG_PROFILE builds: [block][16] phase times (10 ns ticks)
 };
 
@@ -118,6 +120,26 @@ struct WxGroupFinArgs {
   wx_i64 capacity;
   int key_lo;
   const wx_u64 *sorted;  // nullable: general-key entries pre-sorted on the device (> WX_GROUP_HSORT_MAX)
+  // nullable: partials mode (wx_group_partials): the window goes here densely
+  // as [W sums | W counts as f64 | 1 out-of-window group count], and only the
+  // out-of-window groups go to out_keys / out_sums / out_counts
+  double *win_out;
+};
+
+// Final GROUP BY result from a combined exchange window (wx_group_partials
+// layout) and the combined out-of-window groups (ascending keys).
+struct WxGroupCombineArgs {
+  const double *window;  // [2 * WX_GROUP_WINDOW + 1]
+  const int *x_keys;     // [n_extra], ascending, none inside the window
+  const double *x_sums;
+  const wx_i64 *x_counts;
+  wx_i64 n_extra;
+  int key_lo;
+  int *out_keys;
+  double *out_sums;
+  wx_i64 *out_counts;
+  wx_i64 capacity;
+  wx_i64 *n_groups_out;
 };
 
 // General-key entries -> (key ^ sign) << 32 | used-list position, padded
@@ -158,6 +180,14 @@ struct WxFillArgs {
   wx_i64 row_base;
   int dtype;
   int kind;
+};
+
+struct WxCastArgs {
+  const void *src;
+  void *dst;
+  wx_i64 n;
+  int src_dtype;  // wx_dtype numbering (0 int32, 1 int64, 2 float32, 3 float64)
+  int dst_dtype;
 };
 
 struct WxSortPrepArgs {
@@ -215,6 +245,7 @@ struct WxSumFinArgs {
   const wx_u32 *part_max;
   double *out;  // wx_stats: {sum f64, count i64, min f32, max f32} (min/max in WX_MINMAX builds)
   int n_parts;
+  int count_f64;  // write the count as a double (WX_F_F64_COUNTS: all-reduce layout)
 };
 
 #endif  // WX_ARGS_H

@@ -318,7 +318,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 // (g, thread, e) of a tile is at offset g*4*WX_DTHREADS + thread*4 + e, so each group is one 16-byte
 // load per lane per column.  In-tile ranks come from 64-bit wavefront ballots
 // (v_mbcnt) and a WX_DWAVES x WX_GROUPS LDS table.  A tile's global offset comes
-// from its predecessors' 8-byte status words {flag:2 | value:62}; a status
+// from its predecessors' 8-byte status words {epoch:6 | flag:2 | value:56}; a status
 // word is its own payload (single agent-scope 8-byte stores and loads), so no
 // fence is needed, and output rows are never read inside the launch.
 //
@@ -338,9 +338,16 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 #define WX_DTHREADS (WX_DWAVES * 64)
 #define WX_TILE (WX_DTHREADS * 4 * WX_GROUPS)  // rows per tile
 #define WX_CBLOCK (WX_DTHREADS + 64)            // + 1 control wave
-#define WX_FLAG_A (1ull << 62)
-#define WX_FLAG_P (2ull << 62)
-#define WX_VAL_MASK ((1ull << 62) - 1ull)
+// Status word {epoch:6 | flag:2 | value:56}: a word whose epoch is not this
+// launch's reads as "not published", so the host never clears the array
+// between queries (a new epoch per launch; one memset every 63 launches).
+#define WX_FLAG_A (1ull << 56)
+#define WX_FLAG_P (2ull << 56)
+#define WX_VAL_MASK ((1ull << 56) - 1ull)
+#define WX_EPOCH_SHIFT 58
+__device__ __forceinline__ wx_u64 wx_cflag(wx_u64 w, wx_u64 E) {
+  return (w >> WX_EPOCH_SHIFT) == (E >> WX_EPOCH_SHIFT) ? (w >> 56) & 3ull : 0ull;
+}
 #ifndef WX_COMPACT_VSTORE
 #define WX_COMPACT_VSTORE 1  // 16-byte aligned stores for the output runs (2.65 -> 2.47 ms)
 #endif
@@ -349,8 +356,11 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 // process (2.71 vs 2.47 ms, profiles/r01/ablate_compact_ab.txt), kept off
 #define WX_COMPACT_WHOLE_LOADS 0
 #endif
-#ifndef WX_SPIN_LIMIT
-#define WX_SPIN_LIMIT (1u << 20)
+#ifndef WX_STALL_TICKS
+// A waiter gives up after this long (s_memrealtime, 100 MHz) without any
+// polled word changing: progress, not poll count, so a query slowed down by
+// another process sharing the GPU still completes.
+#define WX_STALL_TICKS 200000000ull  // 2 s
 #endif
 #ifndef WX_LB_PER_LANE
 #define WX_LB_PER_LANE 1  // predecessors per lane per look-back round (1 measured fastest: each agent-scope poll is costly)
@@ -375,15 +385,19 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
 // assumption drains the grid quickly instead of hanging it.
 __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 tile) {
   const int lane = threadIdx.x & 63;
+  const wx_u64 E = (wx_u64)a.epoch << WX_EPOCH_SHIFT;
+  const wx_u64 abort_word = E | 1ull;  // flag 0, value 1: never a tile word
   wx_i64 excl = 0;
   wx_i64 look = tile - 1;
   wx_u32 spins = 0;
+  bool moved = false;
+  wx_u64 t_last = 0;
   while (true) {
     wx_u64 st[WX_LB_PER_LANE];
 #pragma unroll
     for (int j = 0; j < WX_LB_PER_LANE; ++j) {
       const wx_i64 t = look - 64 * j - lane;
-      st[j] = t >= 0 ? wx::ld_agent(&a.status[t]) : WX_FLAG_P;  // "tile -1": inclusive 0
+      st[j] = t >= 0 ? wx::ld_agent(&a.status[t]) : (E | WX_FLAG_P);  // "tile -1": inclusive 0
     }
     // Wait only for the entries nearer than the nearest inclusive prefix
     // already visible (distance order (j, lane)); farther ones do not matter.
@@ -393,28 +407,36 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
       bool pending = false;
 #pragma unroll
       for (int j = WX_LB_PER_LANE - 1; j >= 0; --j) {
-        const wx_u64 pm = __builtin_amdgcn_ballot_w64((st[j] >> 62) == 2ull);
+        const wx_u64 pm = __builtin_amdgcn_ballot_w64(wx_cflag(st[j], E) == 2ull);
         if (pm) near_p = 64 * j + __builtin_ctzll(pm);
       }
 #pragma unroll
       for (int j = 0; j < WX_LB_PER_LANE; ++j) {
-        const bool need = (st[j] >> 62) == 0ull && 64 * j + lane < near_p;
+        const bool need = wx_cflag(st[j], E) == 0ull && 64 * j + lane < near_p;
         pending |= __builtin_amdgcn_ballot_w64(need) != 0ull;
       }
       if (!pending) break;
       __builtin_amdgcn_s_sleep(WX_LB_SLEEP);
 #pragma unroll
       for (int j = 0; j < WX_LB_PER_LANE; ++j) {
-        if ((st[j] >> 62) == 0ull && 64 * j + lane < near_p) st[j] = wx::ld_agent(&a.status[look - 64 * j - lane]);
+        if (wx_cflag(st[j], E) == 0ull && 64 * j + lane < near_p) {
+          const wx_u64 w = wx::ld_agent(&a.status[look - 64 * j - lane]);
+          moved |= w != st[j];
+          st[j] = w;
+        }
       }
       if ((++spins & 63u) == 0u) {
-        if (spins > WX_SPIN_LIMIT) {  // sticky error for the host + this launch's abort word
+        const wx_u64 now = __builtin_amdgcn_s_memrealtime();
+        if (__builtin_amdgcn_ballot_w64(moved) != 0ull || t_last == 0ull) {
+          t_last = now;
+          moved = false;
+        } else if (now - t_last > WX_STALL_TICKS) {  // sticky error for the host + this launch's abort word
           atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_LOOKBACK);
-          wx::st_agent(&a.status[a.n_tiles], 1ull);
+          wx::st_agent(&a.status[a.n_tiles], abort_word);
         }
-        if (wx::ld_agent(&a.status[a.n_tiles])) {
+        if (wx::ld_agent(&a.status[a.n_tiles]) == abort_word) {
 #pragma unroll
-          for (int j = 0; j < WX_LB_PER_LANE; ++j) st[j] = WX_FLAG_P;
+          for (int j = 0; j < WX_LB_PER_LANE; ++j) st[j] = E | WX_FLAG_P;
         }
       }
     }
@@ -425,8 +447,20 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
     excl += (wx_i64)wx::wave_sum_u64(v);
     if (near_p < 64 * WX_LB_PER_LANE) break;
     look -= 64 * WX_LB_PER_LANE;
+    t_last = 0ull;  // the window moved: progress
   }
   return excl;
+}
+
+// The last workgroup of a compaction launch to retire returns the tile
+// ticket to 0 for the next launch on this workspace (no host memset per
+// query).  Every workgroup calls it once after its last ticket fetch.
+__device__ __forceinline__ void wx_retire(wx_u64 *ctrs) {
+  const wx_u64 done = __hip_atomic_fetch_add(&ctrs[2], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  if (done == (wx_u64)gridDim.x - 1ull) {
+    __hip_atomic_store(&ctrs[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctrs[2], 0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+  }
 }
 
 // Evaluate one tile held in wx_in* registers and rank its passing rows.
@@ -491,6 +525,7 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
 #define WX_COMPACT_MINBLOCKS 1  // workgroups per CU the register budget must allow
 #endif
 extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx_project_compact(WxCompactArgs wx_a) {
+  const wx_u64 wx_E = (wx_u64)wx_a.epoch << WX_EPOCH_SHIFT;
   __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
   __shared__ float s_val[WX_TILE];
   __shared__ unsigned short s_off[WX_TILE];
@@ -587,7 +622,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     if (have) { WX_BASES(s_cnt) }
     if (control) {
       if (have && lane == 0)
-        wx::st_agent(&wx_a.status[tile], (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
+        wx::st_agent(&wx_a.status[tile], wx_E | (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
 #if WX_COMPACT_TICKETS
       // the tile of iteration k + 2 (slot last read as `prev` in iteration k - 1)
       if (lane == 0)
@@ -662,7 +697,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #else
         if (tile > 0) {
           excl = wx_lookback(wx_a, tile);
-          if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_P | (wx_u64)(excl + block_total));
+          if (lane == 0) wx::st_agent(&wx_a.status[tile], wx_E | WX_FLAG_P | (wx_u64)(excl + block_total));
         }
 #endif
         if (lane == 0) {
@@ -689,6 +724,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     prev_tile = tile;
     tile = next_tile;
   }
+  if (tid == 0) wx_retire(wx_a.ctrs);
 #if WX_DIAG_PROFILE
   if (wx_a.diag && (tid == 0 || tid == WX_DTHREADS)) {
     wx_u64 *d = wx_a.diag + (wx_u64)blockIdx.x * 16 + (tid == 0 ? 0 : 8);
@@ -711,6 +747,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #endif
 #if defined(WX_COMPACT_STATIC) && WX_COMPACT_STATIC == 3
 extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx_project_compact_deep(WxCompactArgs wx_a) {
+  const wx_u64 wx_E = (wx_u64)wx_a.epoch << WX_EPOCH_SHIFT;
   __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
   __shared__ float s_val[2][WX_TILE];
   __shared__ unsigned short s_off[2][WX_TILE];
@@ -787,7 +824,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     if (have) { WX_BASES(s_cnt) }
     if (control) {
       if (lane == 0) {
-        if (have) wx::st_agent(&wx_a.status[tile], (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
+        if (have) wx::st_agent(&wx_a.status[tile], wx_E | (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
         s_tiles[(k + 2) & 3] = next_tile < wx_a.n_tiles
                                    ? (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED,
                                                                     __HIP_MEMORY_SCOPE_AGENT)
@@ -847,7 +884,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
         wx_i64 excl = 0;
         if (tile1 > 0) {
           excl = wx_lookback(wx_a, tile1);
-          if (lane == 0) wx::st_agent(&wx_a.status[tile1], WX_FLAG_P | (wx_u64)(excl + tot1));
+          if (lane == 0) wx::st_agent(&wx_a.status[tile1], wx_E | WX_FLAG_P | (wx_u64)(excl + tot1));
         }
         if (lane == 0) {
           s_excl[cur ^ 1] = excl;  // read when t_{k-1} is written, in iteration k + 1
@@ -874,11 +911,13 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     tot1 = have ? block_total : 0u;
     tile = next_tile;
   }
+  if (tid == 0) wx_retire(wx_a.ctrs);
 }
 #endif
 
 // One tile per workgroup, taken from a ticket counter (robust fallback).
 extern "C" __global__ __launch_bounds__(WX_DTHREADS) void wx_project_compact_ticket(WxCompactArgs wx_a) {
+  const wx_u64 wx_E = (wx_u64)wx_a.epoch << WX_EPOCH_SHIFT;
   __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
   __shared__ wx_i64 s_excl;
   __shared__ wx_u32 s_tile;
@@ -906,11 +945,11 @@ extern "C" __global__ __launch_bounds__(WX_DTHREADS) void wx_project_compact_tic
   if (wave == 0) {
     wx_i64 excl = 0;
     if (tile == 0) {
-      if (lane == 0) wx::st_agent(&wx_a.status[0], WX_FLAG_P | (wx_u64)block_total);
+      if (lane == 0) wx::st_agent(&wx_a.status[0], wx_E | WX_FLAG_P | (wx_u64)block_total);
     } else {
-      if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_A | (wx_u64)block_total);
+      if (lane == 0) wx::st_agent(&wx_a.status[tile], wx_E | WX_FLAG_A | (wx_u64)block_total);
       excl = wx_lookback(wx_a, tile);
-      if (lane == 0) wx::st_agent(&wx_a.status[tile], WX_FLAG_P | (wx_u64)(excl + block_total));
+      if (lane == 0) wx::st_agent(&wx_a.status[tile], wx_E | WX_FLAG_P | (wx_u64)(excl + block_total));
     }
     if (lane == 0) s_excl = excl;
   }
@@ -934,6 +973,7 @@ extern "C" __global__ __launch_bounds__(WX_DTHREADS) void wx_project_compact_tic
     }
   }
   if (tid == 0 && tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
+  if (tid == 0) wx_retire(wx_a.ctrs);
 }
 #endif
 
@@ -1069,7 +1109,8 @@ extern "C" __global__ __launch_bounds__(WX_SFIN_BLOCK) void wx_sum_finalize(WxSu
       tmx = s_max[w] > tmx ? s_max[w] : tmx;
     }
     a.out[0] = ts;
-    reinterpret_cast<wx_i64 *>(a.out)[1] = tc;
+    if (a.count_f64) a.out[1] = (double)tc;  // exact below 2^53
+    else reinterpret_cast<wx_i64 *>(a.out)[1] = tc;
     if (WX_MINMAX) {
       reinterpret_cast<float *>(a.out)[4] = wx::minmax_out(tmn, true);
       reinterpret_cast<float *>(a.out)[5] = wx::minmax_out(tmx, false);
@@ -1251,9 +1292,12 @@ extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(Wx
   }
   __syncthreads();
   const wx_i64 nlo = s_nlo;
-  // dense window compaction (ascending bins): wave scan + wave totals
+  // dense window compaction (ascending bins): wave scan + wave totals;
+  // partials mode exports the window densely instead (f = 0: no window group
+  // takes an output slot, so the out-of-window groups land at 0..nh)
+  const bool part = a.win_out != nullptr;
   const int lane = tid & 63, wave = tid >> 6;
-  const wx_u32 f = (wc0 ? 1u : 0u) + (wc1 ? 1u : 0u);
+  const wx_u32 f = part ? 0u : (wc0 ? 1u : 0u) + (wc1 ? 1u : 0u);
   wx_u32 incl = f;
 #pragma unroll
   for (int o = 1; o < 64; o <<= 1) {
@@ -1275,6 +1319,14 @@ extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(Wx
     for (int h = 0; h < 2; ++h) {
       const int b = b0 + h;
       const wx_u64 c = h ? wc1 : wc0;
+      if (part) {
+        a.win_out[b] = c ? a.win_sum[b] : 0.0;
+        a.win_out[WX_GWIN + b] = (double)c;
+        if (!c) continue;
+        a.win_sum[b] = 0.0;
+        a.win_cnt[b] = 0ull;
+        continue;
+      }
       if (!c) continue;
       if (pos < a.capacity) {
         a.out_keys[pos] = a.key_lo + b;
@@ -1326,6 +1378,7 @@ extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(Wx
   if (tid == 0) {
     a.ctrs[0] = 0ull;
     *a.n_groups_out = too_many ? -1 : total;
+    if (part) a.win_out[2 * WX_GWIN] = too_many ? 0.0 : (double)total;
     if (total > a.capacity) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_CAPACITY);
   }
 #undef WX_ENT
@@ -1675,6 +1728,98 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_fill_synthetic(WxFillA
   }
 }
 
+// Final GROUP BY result of a row-sharded query (query_multi_gpu GROUP BY):
+// the combined exchange window (sums, counts as f64 -- element-wise sums of
+// every shard's wx_group_partials window) and the combined out-of-window
+// groups (ascending keys) merged in ascending key order: the groups below
+// the window, the non-empty window bins, the groups above.  One 1024-thread
+// block, two window bins per thread, ranked by a block scan (as
+// wx_group_finalize).
+#define WX_GCOMB_BLOCK 1024
+static_assert(WX_GROUP_WINDOW == 2 * WX_GCOMB_BLOCK, "two window bins per combine thread");
+extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine(WxGroupCombineArgs a) {
+  __shared__ wx_u32 s_wtot[WX_GCOMB_BLOCK / 64];
+  __shared__ wx_i64 s_nlo;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b0 = 2 * tid;
+  const double c0 = a.window[WX_GROUP_WINDOW + b0], c1 = a.window[WX_GROUP_WINDOW + b0 + 1];
+  if (tid == 0) {  // out-of-window groups below the window
+    wx_i64 lo = 0, hi = a.n_extra;
+    while (lo < hi) {
+      const wx_i64 mid = (lo + hi) >> 1;
+      if (a.x_keys[mid] < a.key_lo) lo = mid + 1;
+      else hi = mid;
+    }
+    s_nlo = lo;
+  }
+  const wx_u32 f = (c0 != 0.0 ? 1u : 0u) + (c1 != 0.0 ? 1u : 0u);
+  wx_u32 incl = f;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const wx_u32 t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_wtot[wave] = incl;
+  __syncthreads();
+  wx_u32 wbase = 0, wsum = 0;
+#pragma unroll
+  for (int w = 0; w < WX_GCOMB_BLOCK / 64; ++w) {
+    const wx_u32 v = s_wtot[w];
+    wbase += (w < wave) ? v : 0u;
+    wsum += v;
+  }
+  const wx_i64 nlo = s_nlo;
+  wx_i64 pos = nlo + wbase + incl - f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int b = b0 + h;
+    const double c = h ? c1 : c0;
+    if (c == 0.0) continue;
+    if (pos < a.capacity) {
+      a.out_keys[pos] = a.key_lo + b;
+      a.out_sums[pos] = a.window[b];
+      a.out_counts[pos] = (wx_i64)c;
+    }
+    ++pos;
+  }
+  const wx_i64 above = nlo + wsum;
+  for (wx_i64 i = tid; i < a.n_extra; i += WX_GCOMB_BLOCK) {
+    const wx_i64 p = i < nlo ? i : above + (i - nlo);
+    if (p < a.capacity) {
+      a.out_keys[p] = a.x_keys[i];
+      a.out_sums[p] = a.x_sums[i];
+      a.out_counts[p] = a.x_counts[i];
+    }
+  }
+  if (tid == 0) *a.n_groups_out = above + (a.n_extra - nlo);
+}
+
+// Element-wise C conversion between the column types (wx_cast), e.g. the
+// double GROUP BY sums into the float outputs of jit_group_sum.
+template <typename S, typename D>
+__device__ __forceinline__ void wx_cast_loop(const void *src, void *dst, wx_i64 n) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < n; i += stride)
+    static_cast<D *>(dst)[i] = (D) static_cast<const S *>(src)[i];
+}
+template <typename S>
+__device__ __forceinline__ void wx_cast_to(const WxCastArgs &a) {
+  switch (a.dst_dtype) {
+    case 0: wx_cast_loop<S, int>(a.src, a.dst, a.n); break;
+    case 1: wx_cast_loop<S, wx_i64>(a.src, a.dst, a.n); break;
+    case 2: wx_cast_loop<S, float>(a.src, a.dst, a.n); break;
+    default: wx_cast_loop<S, double>(a.src, a.dst, a.n); break;
+  }
+}
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
+  switch (a.src_dtype) {
+    case 0: wx_cast_to<int>(a); break;
+    case 1: wx_cast_to<wx_i64>(a); break;
+    case 2: wx_cast_to<float>(a); break;
+    default: wx_cast_to<double>(a); break;
+  }
+}
+
 // kind 0: float values, kind 1: int keys.  Descending order inverts the rank
 // but not the position, so equal keys keep their input order (stable).
 extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_prep(WxSortPrepArgs a) {
@@ -1776,8 +1921,8 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApply
 #ifndef WX_RS_LBW
 #define WX_RS_LBW 1  // predecessor words per digit per look-back round (8 measured slower: poll traffic)
 #endif
-#ifndef WX_SPIN_LIMIT
-#define WX_SPIN_LIMIT (1u << 20)
+#ifndef WX_STALL_TICKS
+#define WX_STALL_TICKS 200000000ull  // 2 s at 100 MHz without progress (see the compaction look-back)
 #endif
 #define WX_RS_FLAG_A (1ull << 56)
 #define WX_RS_FLAG_P (2ull << 56)
@@ -2053,6 +2198,7 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
       // the first unpublished word (re-polled from there) or the first {P}
       wx_i64 p = (wx_i64)tile - 1;
       wx_u32 spins = 0;
+      wx_u64 t_last = 0ull;  // time of the last progress (0: not yet sampled)
       bool fresh = WX_RS_LB_FIRST;
       while (true) {
         wx_u64 wv[WX_RS_LBW];
@@ -2079,12 +2225,18 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
         if (done) break;
         if (stop == WX_RS_LBW) {
           p -= WX_RS_LBW;
+          t_last = 0ull;  // progress
           continue;
         }
+        if (stop > 0) t_last = 0ull;
         p -= stop;
         __builtin_amdgcn_s_sleep(1);
         if ((++spins & 63u) == 0u) {
-          if (spins > WX_SPIN_LIMIT) {
+          // abort only after WX_STALL_TICKS with this digit's chain not moving
+          const wx_u64 now = __builtin_amdgcn_s_memrealtime();
+          if (t_last == 0ull) {
+            t_last = now;
+          } else if (now - t_last > WX_STALL_TICKS) {
             atomicOr(a.err, WX_DEVERR_LOOKBACK);
             atomicExch(&a.ctl[1], 1u);
           }

@@ -3,7 +3,11 @@
 // failure with the reference's messages (src/jit.cpp:11-28, :123-129).
 #include <hip/hip_runtime_api.h>
 
+#include <algorithm>
 #include <iostream>
+#include <map>
+#include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -56,6 +60,26 @@ void jit_compile_and_launch(const std::string &expr_code, const std::string &con
            err);
 }
 
+namespace {
+// Double sums / int64 counts behind jit_group_sum, per device, kept across
+// calls and grown only when a query has more groups than it holds: O(groups)
+// of HBM, not O(rows) (the reference's caller sizes its outputs for N rows,
+// src/warpdb.cpp:356-358, but a GROUP BY yields at most a few thousand).
+struct GroupScratch {
+  std::mutex mu;
+  DeviceBuffer sums, counts;
+  int64_t cap = 0;
+};
+GroupScratch &group_scratch(int device) {
+  static std::mutex mu;
+  static auto *all = new std::map<int, std::unique_ptr<GroupScratch>>();  // never destroyed (HIP teardown order)
+  std::lock_guard<std::mutex> lk(mu);
+  auto &p = (*all)[device];
+  if (!p) p.reset(new GroupScratch);
+  return *p;
+}
+}  // namespace
+
 void jit_group_sum(const std::string &val_expr_code, const std::string &key_expr_code, float *d_price,
                    int *d_quantity, float *d_out_vals, int *d_out_keys, int *d_count, int N, int device_id) {
   // the reference kernel binds exactly these two columns (src/jit.cpp:194)
@@ -66,22 +90,34 @@ void jit_group_sum(const std::string &val_expr_code, const std::string &key_expr
   t.columns.push_back({"quantity", DataType::Int32, d_quantity, N});
   WxTableView v(t);
   wx_launch L = sync_launch(device_id);
-  const int64_t cap = N > 0 ? N : 1;
-  DeviceBuffer sums(device_id, cap * sizeof(double)), counts(device_id, cap * sizeof(int64_t));
+  GroupScratch &scr = group_scratch(device_id);
+  std::lock_guard<std::mutex> lk(scr.mu);
+  int64_t cap = std::max<int64_t>(scr.cap, 4096);
   int64_t groups = 0;
   char err[8192];
-  throw_on(wx_group_sum(&v.table, val_expr_code.c_str(), key_expr_code.c_str(), nullptr, &L, 0, cap, d_out_keys,
-                        static_cast<double *>(sums.ptr), static_cast<int64_t *>(counts.ptr), nullptr, &groups, err,
-                        sizeof(err)),
-           err);
-  // the reference's outputs are float sums and an int count
-  std::vector<double> h(static_cast<size_t>(groups));
+  for (;;) {
+    if (scr.cap < cap) {
+      scr.sums = DeviceBuffer();
+      scr.counts = DeviceBuffer();
+      scr.sums = DeviceBuffer(device_id, cap * sizeof(double));
+      scr.counts = DeviceBuffer(device_id, cap * sizeof(int64_t));
+      scr.cap = cap;
+    }
+    const wx_status st = wx_group_sum(&v.table, val_expr_code.c_str(), key_expr_code.c_str(), nullptr, &L, 0, cap,
+                                      d_out_keys, static_cast<double *>(scr.sums.ptr),
+                                      static_cast<int64_t *>(scr.counts.ptr), nullptr, &groups, err, sizeof(err));
+    if (st == WX_ERR_CAPACITY) {  // more groups than the scratch holds: grow and run again
+      cap = std::max<int64_t>(2 * cap, groups + 1);
+      continue;
+    }
+    throw_on(st, err);
+    break;
+  }
+  // the reference's outputs are float sums and an int count: converted on
+  // the device, nothing but the count crosses to the host
+  throw_on(wx_cast(scr.sums.ptr, WX_FLOAT64, d_out_vals, WX_FLOAT32, groups, &L, err, sizeof(err)), err);
   DevGuard g(device_id);
-  if (groups) hip_ok(hipMemcpy(h.data(), sums.ptr, groups * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
-  std::vector<float> f(h.begin(), h.end());
-  if (groups) hip_ok(hipMemcpy(d_out_vals, f.data(), groups * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy");
-  const int gc = static_cast<int>(groups);
-  hip_ok(hipMemcpy(d_count, &gc, sizeof(int), hipMemcpyHostToDevice), "hipMemcpy");
+  hip_ok(hipMemsetD32(reinterpret_cast<hipDeviceptr_t>(d_count), static_cast<int>(groups), 1), "hipMemsetD32");
 }
 
 void jit_sort_pairs(int *d_keys, float *d_vals, int count, bool ascending, int device_id) {

@@ -3,9 +3,10 @@
 //
 // One host thread per device uploads its shard, launches on its own stream
 // and downloads its slice of the result, so the devices run concurrently.
-// The only cross-device exchange is the final aggregate of
-// run_multi_gpu_sum: one RCCL all-reduce over a communicator built once with
-// ncclCommInitAll (xGMI on MI355X nodes).
+// The cross-device exchanges are the aggregates' (SURVEY.md 8(e)), each ONE
+// RCCL all-reduce over a communicator built once with ncclCommInitAll (xGMI
+// on MI355X nodes): SUM {sum, count} as two doubles, GROUP BY the 4097-double
+// key window of wx_group_partials.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
@@ -49,13 +50,27 @@ int device_count() {
   return n;
 }
 
+// `want` devices (0 = every visible one), checked against what is there
+int devices_for(int want) {
+  const int have = device_count();
+  if (want <= 0) return have;
+  if (want > have) throw std::runtime_error("requested " + std::to_string(want) + " devices, " +
+                                            std::to_string(have) + " visible");
+  return want;
+}
+
 size_t width(DataType t) { return (t == DataType::Int64 || t == DataType::Float64) ? 8 : 4; }
 
-// Device copy of rows [b, e) of every numeric column.
+}  // namespace
+
+// Device copy of rows [b, e) of every numeric column (bufs empty: the
+// columns are borrowed from a Table the caller keeps alive).
 struct Shard {
   std::vector<DeviceBuffer> bufs;
   Table table;
 };
+
+namespace {
 
 Shard upload_shard(const HostTable &h, int device, int64_t b, int64_t e, hipStream_t s) {
   Shard sh;
@@ -153,6 +168,27 @@ Comms &comms_for(int ndev) {
 
 namespace {
 
+// In-place ncclAllReduce(SUM, ncclFloat64) of `count` doubles of every
+// shard's buffer, one call per device inside one group (devices 0..n-1, as
+// plan_shards assigns them).  A single shard has nothing to exchange.
+void allreduce_f64(const std::vector<ShardRange> &shards, const std::vector<double *> &bufs,
+                   const std::vector<hipStream_t> &streams, size_t count) {
+  const int nshard = static_cast<int>(shards.size());
+  if (nshard < 2) return;
+  Comms &c = comms_for(nshard);
+  std::lock_guard<std::mutex> lk(c.mu);
+  if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
+  for (int i = 0; i < nshard; ++i) {
+    DevGuard g(shards[i].device);
+    double *p = bufs[i];
+    if (ncclAllReduce(p, p, count, ncclFloat64, ncclSum, c.comms[i], streams[i]) != ncclSuccess) {
+      (void)ncclGroupEnd();
+      throw std::runtime_error("ncclAllReduce failed");
+    }
+  }
+  if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("RCCL all-reduce failed");
+}
+
 // SUM over shards already in HBM: one reduce per device, then one RCCL
 // all-reduce of {sum (f64), count (i64)} across the shards' devices.
 std::pair<double, int64_t> sum_over_shards(const std::vector<ShardRange> &shards, std::vector<Shard> &keep,
@@ -167,25 +203,16 @@ std::pair<double, int64_t> sum_over_shards(const std::vector<ShardRange> &shards
     outs[i] = DeviceBuffer(r.device, 16);
     WxTableView v(keep[i].table);
     wx_launch L = sync_launch(r.device, streams[i]);
-    L.flags = 0;  // asynchronous; synchronised after the collective
+    L.flags = WX_F_F64_COUNTS;  // {sum, count} as two doubles; asynchronous until after the collective
     char err[8192];
     throw_on(wx_reduce_sum(&v.table, expr_cuda.c_str(), cond_cuda.c_str(), &L, outs[i].ptr, nullptr, nullptr, err,
                            sizeof(err)),
              err);
   });
   const int nshard = static_cast<int>(shards.size());
-  Comms &c = comms_for(nshard);
-  {
-    std::lock_guard<std::mutex> lk(c.mu);
-    if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
-    for (int i = 0; i < nshard; ++i) {
-      DevGuard g(shards[i].device);
-      double *p = static_cast<double *>(outs[i].ptr);
-      ncclAllReduce(p, p, 1, ncclFloat64, ncclSum, c.comms[i], streams[i]);
-      ncclAllReduce(p + 1, p + 1, 1, ncclInt64, ncclSum, c.comms[i], streams[i]);
-    }
-    if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("RCCL all-reduce failed");
-  }
+  std::vector<double *> ptrs;
+  for (auto &o : outs) ptrs.push_back(static_cast<double *>(o.ptr));
+  allreduce_f64(shards, ptrs, streams, 2);
   double res[2] = {0, 0};
   for (int i = 0; i < nshard; ++i) {
     DevGuard g(shards[i].device);
@@ -195,9 +222,7 @@ std::pair<double, int64_t> sum_over_shards(const std::vector<ShardRange> &shards
     throw_on(wx_check(&L, err, sizeof(err)), err);
     if (i == 0) hip_ok(hipMemcpy(res, outs[i].ptr, 16, hipMemcpyDeviceToHost), "hipMemcpy");
   }
-  int64_t cnt;
-  std::memcpy(&cnt, &res[1], 8);
-  return {res[0], cnt};
+  return {res[0], static_cast<int64_t>(res[1])};
 }
 
 }  // namespace
@@ -215,16 +240,25 @@ std::pair<double, int64_t> run_multi_gpu_sum(const HostTable &host, const std::s
 }
 
 // ------------------------------------------------------- resident shards
+// Per-shard device buffers of the GROUP BY exchange, kept across queries.
+struct GroupScratch {
+  int64_t cap = 0;
+  DeviceBuffer win, xk, xs, xc, nx, ok, os, oc, ng;
+};
+
 struct ResidentShards::Impl {
   int64_t n = 0;
   std::vector<ShardRange> ranges;
   std::vector<Shard> shards;
+  std::vector<GroupScratch> group;
   std::mutex mu;  // one query at a time per object (shared workspaces and scratch)
 };
 
-ResidentShards::ResidentShards(const HostTable &host) : impl_(new Impl) {
+ResidentShards::ResidentShards() : impl_(new Impl) {}
+
+ResidentShards::ResidentShards(const HostTable &host, int devices) : impl_(new Impl) {
   impl_->n = host.num_rows();
-  impl_->ranges = plan_shards(impl_->n, device_count());
+  impl_->ranges = plan_shards(impl_->n, devices_for(devices));
   impl_->shards.resize(impl_->ranges.size());
   run_per_device(impl_->ranges, [&](size_t i, const ShardRange &r) {
     hipStream_t s = device_stream(r.device);
@@ -233,14 +267,59 @@ ResidentShards::ResidentShards(const HostTable &host) : impl_(new Impl) {
   });
 }
 
+std::unique_ptr<ResidentShards> ResidentShards::borrow(const Table &table) {
+  std::unique_ptr<ResidentShards> r(new ResidentShards());
+  r->impl_->n = table.num_rows;
+  if (table.num_rows > 0) {
+    r->impl_->ranges.push_back({table.device, 0, table.num_rows});
+    r->impl_->shards.resize(1);
+    r->impl_->shards[0].table = table;  // column pointers only; the caller owns the memory
+  }
+  return r;
+}
+
+std::unique_ptr<ResidentShards> ResidentShards::synthetic(int64_t n_rows, const std::vector<SyntheticColumn> &cols,
+                                                          int devices) {
+  std::unique_ptr<ResidentShards> r(new ResidentShards());
+  Impl &im = *r->impl_;
+  im.n = n_rows;
+  im.ranges = plan_shards(n_rows, devices_for(devices));
+  im.shards.resize(im.ranges.size());
+  run_per_device(im.ranges, [&](size_t i, const ShardRange &sr) {
+    hipStream_t s = device_stream(sr.device);
+    Shard &sh = im.shards[i];
+    const int64_t rows = sr.end - sr.begin;
+    sh.table.num_rows = rows;
+    sh.table.device = sr.device;
+    for (const auto &c : cols) {
+      if (c.type == DataType::String) throw std::runtime_error("synthetic string columns are not supported");
+      sh.bufs.emplace_back(sr.device, width(c.type) * static_cast<size_t>(rows));
+      wx_launch L = sync_launch(sr.device, s);
+      char err[1024];
+      // rows are generated at their global row numbers: every shard holds
+      // exactly the rows a single-device table would have
+      throw_on(wx_fill_synthetic(sh.bufs.back().ptr, static_cast<int32_t>(c.type), rows, c.seed, c.kind, c.lo, c.hi,
+                                 sr.begin, &L, err, sizeof(err)),
+               err);
+      sh.table.columns.push_back({c.name, c.type, sh.bufs.back().ptr, rows});
+    }
+  });
+  return r;
+}
+
 ResidentShards::~ResidentShards() {
   for (size_t i = 0; i < impl_->shards.size(); ++i) {
     DevGuard g(impl_->ranges[i].device);
     impl_->shards[i] = Shard();
+    if (i < impl_->group.size()) impl_->group[i] = GroupScratch();
   }
 }
 
 int64_t ResidentShards::num_rows() const { return impl_->n; }
+
+int ResidentShards::num_shards() const { return static_cast<int>(impl_->ranges.size()); }
+
+std::vector<ShardRange> ResidentShards::ranges() const { return impl_->ranges; }
 
 std::vector<float> ResidentShards::dense(const std::string &expr_cuda, const std::string &cond_cuda) const {
   std::lock_guard<std::mutex> lk(impl_->mu);
@@ -273,6 +352,132 @@ std::vector<float> ResidentShards::dense(const std::string &expr_cuda, const std
 std::pair<double, int64_t> ResidentShards::sum(const std::string &expr_cuda, const std::string &cond_cuda) const {
   std::lock_guard<std::mutex> lk(impl_->mu);
   return sum_over_shards(impl_->ranges, impl_->shards, expr_cuda, cond_cuda, nullptr);
+}
+
+// GROUP BY over the shards: per device wx_group_partials
+// (dense 2048-key window + out-of-window groups), ONE ncclAllReduce of the
+// 4097-double windows, then wx_group_combine on the first shard's device.
+// Groups outside the window (rare: keys spread wider than 2048 values) are
+// read back from every shard and merged on the host before the combine.
+GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::string &key_cuda,
+                                      const std::string &cond_cuda, int32_t key_lo) const {
+  std::lock_guard<std::mutex> lk(impl_->mu);
+  GroupResult res;
+  const auto &ranges = impl_->ranges;
+  const size_t ns = ranges.size();
+  if (ns == 0) return res;
+  constexpr int64_t kCap = 1 << 16;  // out-of-window groups per shard / final groups
+  constexpr size_t W = WX_GROUP_WINDOW_BINS, WD = WX_GROUP_EXCHANGE_DOUBLES;
+  if (impl_->group.size() < ns) impl_->group.resize(ns);
+  std::vector<double *> wins(ns, nullptr);
+  std::vector<hipStream_t> streams(ns, nullptr);
+  run_per_device(ranges, [&](size_t i, const ShardRange &r) {
+    streams[i] = device_stream(r.device);
+    GroupScratch &g = impl_->group[i];
+    if (g.cap < kCap) {
+      g.win = DeviceBuffer(r.device, WD * 8);
+      g.xk = DeviceBuffer(r.device, kCap * 4);
+      g.xs = DeviceBuffer(r.device, kCap * 8);
+      g.xc = DeviceBuffer(r.device, kCap * 8);
+      g.nx = DeviceBuffer(r.device, 8);
+      g.ok = DeviceBuffer(r.device, kCap * 4);
+      g.os = DeviceBuffer(r.device, kCap * 8);
+      g.oc = DeviceBuffer(r.device, kCap * 8);
+      g.ng = DeviceBuffer(r.device, 8);
+      g.cap = kCap;
+    }
+    WxTableView v(impl_->shards[i].table);
+    wx_launch L = sync_launch(r.device, streams[i]);
+    L.flags = 0;  // asynchronous until after the collective
+    char err[8192];
+    throw_on(wx_group_partials(&v.table, val_cuda.c_str(), key_cuda.c_str(), cond_cuda.c_str(), &L, key_lo,
+                               static_cast<double *>(g.win.ptr), kCap, static_cast<int32_t *>(g.xk.ptr),
+                               static_cast<double *>(g.xs.ptr), static_cast<int64_t *>(g.xc.ptr),
+                               static_cast<int64_t *>(g.nx.ptr), nullptr, err, sizeof(err)),
+             err);
+    wins[i] = static_cast<double *>(g.win.ptr);
+  });
+  allreduce_f64(ranges, wins, streams, WD);
+  GroupScratch &g0 = impl_->group[0];
+  const int dev0 = ranges[0].device;
+  char err[8192];
+  wx_launch L0 = sync_launch(dev0, streams[0]);
+  L0.flags = 0;
+  throw_on(wx_group_combine(static_cast<double *>(g0.win.ptr), key_lo, nullptr, nullptr, nullptr, 0, &L0, kCap,
+                            static_cast<int32_t *>(g0.ok.ptr), static_cast<double *>(g0.os.ptr),
+                            static_cast<int64_t *>(g0.oc.ptr), static_cast<int64_t *>(g0.ng.ptr), nullptr, err,
+                            sizeof(err)),
+           err);
+  for (size_t i = 0; i < ns; ++i) {  // every shard's device errors (and the collective) complete
+    DevGuard dg(ranges[i].device);
+    hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
+    wx_launch L = sync_launch(ranges[i].device, streams[i]);
+    throw_on(wx_check(&L, err, sizeof(err)), err);
+  }
+  double n_extra_total = 0;
+  {
+    DevGuard dg(dev0);
+    hip_ok(hipMemcpy(&n_extra_total, static_cast<double *>(g0.win.ptr) + 2 * W, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+  }
+  DeviceBuffer mk, ms, mc;
+  if (n_extra_total > 0) {
+    std::map<int32_t, std::pair<double, int64_t>> merged;
+    for (size_t i = 0; i < ns; ++i) {
+      GroupScratch &g = impl_->group[i];
+      DevGuard dg(ranges[i].device);
+      int64_t nx = 0;
+      hip_ok(hipMemcpy(&nx, g.nx.ptr, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+      std::vector<int32_t> k(nx);
+      std::vector<double> sm(nx);
+      std::vector<int64_t> c(nx);
+      if (nx) {
+        hip_ok(hipMemcpy(k.data(), g.xk.ptr, nx * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+        hip_ok(hipMemcpy(sm.data(), g.xs.ptr, nx * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+        hip_ok(hipMemcpy(c.data(), g.xc.ptr, nx * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+      }
+      for (int64_t j = 0; j < nx; ++j) {
+        auto &e = merged[k[j]];
+        e.first += sm[j];
+        e.second += c[j];
+      }
+    }
+    const int64_t m = static_cast<int64_t>(merged.size());
+    std::vector<int32_t> k;
+    std::vector<double> sm;
+    std::vector<int64_t> c;
+    for (auto &e : merged) {
+      k.push_back(e.first);
+      sm.push_back(e.second.first);
+      c.push_back(e.second.second);
+    }
+    mk = DeviceBuffer(dev0, m * 4);
+    ms = DeviceBuffer(dev0, m * 8);
+    mc = DeviceBuffer(dev0, m * 8);
+    DevGuard dg(dev0);
+    hip_ok(hipMemcpy(mk.ptr, k.data(), m * 4, hipMemcpyHostToDevice), "hipMemcpy");
+    hip_ok(hipMemcpy(ms.ptr, sm.data(), m * 8, hipMemcpyHostToDevice), "hipMemcpy");
+    hip_ok(hipMemcpy(mc.ptr, c.data(), m * 8, hipMemcpyHostToDevice), "hipMemcpy");
+    wx_launch L = sync_launch(dev0, streams[0]);
+    throw_on(wx_group_combine(static_cast<double *>(g0.win.ptr), key_lo, static_cast<int32_t *>(mk.ptr),
+                              static_cast<double *>(ms.ptr), static_cast<int64_t *>(mc.ptr), m, &L, kCap,
+                              static_cast<int32_t *>(g0.ok.ptr), static_cast<double *>(g0.os.ptr),
+                              static_cast<int64_t *>(g0.oc.ptr), static_cast<int64_t *>(g0.ng.ptr), nullptr, err,
+                              sizeof(err)),
+             err);
+  }
+  DevGuard dg(dev0);
+  int64_t ng = 0;
+  hip_ok(hipMemcpy(&ng, g0.ng.ptr, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+  if (ng > kCap) throw std::runtime_error("group table / output capacity exceeded");
+  res.keys.resize(ng);
+  res.sums.resize(ng);
+  res.counts.resize(ng);
+  if (ng) {
+    hip_ok(hipMemcpy(res.keys.data(), g0.ok.ptr, ng * 4, hipMemcpyDeviceToHost), "hipMemcpy");
+    hip_ok(hipMemcpy(res.sums.data(), g0.os.ptr, ng * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+    hip_ok(hipMemcpy(res.counts.data(), g0.oc.ptr, ng * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+  }
+  return res;
 }
 
 }  // namespace warpdb

@@ -40,6 +40,13 @@ warpdb::StatsMap stats_from_dict(const py::dict &d) {
   }
   return m;
 }
+// (keys int32, sums float64, counts int64) as numpy arrays
+py::tuple group_arrays(const warpdb::GroupResult &g) {
+  return py::make_tuple(py::array_t<int32_t>(static_cast<py::ssize_t>(g.keys.size()), g.keys.data()),
+                        py::array_t<double>(static_cast<py::ssize_t>(g.sums.size()), g.sums.data()),
+                        py::array_t<int64_t>(static_cast<py::ssize_t>(g.counts.size()), g.counts.data()));
+}
+
 py::tuple arrow_capsules(ArrowArray *arr, ArrowSchema *schema) {
   py::capsule a(arr, [](void *p) {
     auto *x = static_cast<ArrowArray *>(p);
@@ -95,6 +102,18 @@ PYBIND11_MODULE(pywarpdb, m) {
       .def("query_sum", &WarpDB::query_sum, py::call_guard<py::gil_scoped_release>())
       .def("query_multi_gpu_sum", &WarpDB::query_multi_gpu_sum, py::call_guard<py::gil_scoped_release>())
       .def(
+          "query_multi_gpu_group",
+          [](WarpDB &db, const std::string &sql, int32_t key_lo) {
+            warpdb::GroupResult g;
+            {
+              py::gil_scoped_release nogil;
+              g = db.query_multi_gpu_group(sql, key_lo);
+            }
+            return group_arrays(g);
+          },
+          py::arg("sql"), py::arg("key_window_lo") = 0,
+          "GROUP BY over every GPU (one RCCL all-reduce of the key window) -> (keys, sums, counts).")
+      .def(
           "column_stats",
           [](const WarpDB &db) {
             warpdb::StatsMap m;
@@ -129,6 +148,47 @@ PYBIND11_MODULE(pywarpdb, m) {
         for (const auto &c : db.table().columns) n.push_back(c.name);
         return n;
       });
+
+  // Row shards resident across GPUs (the single-process multi-GPU path:
+  // ncclCommInitAll over devices 0..n-1).  Expressions are lowered C
+  // strings, as the jit_* entry points take them.
+  py::class_<warpdb::ResidentShards>(m, "ResidentShards")
+      .def_static(
+          "synthetic",
+          [](int64_t n_rows, const std::vector<py::tuple> &cols, int devices) {
+            std::vector<warpdb::SyntheticColumn> sc;
+            for (const auto &t : cols)
+              sc.push_back({t[0].cast<std::string>(), t[1].cast<DataType>(), t[2].cast<uint64_t>(), t[3].cast<int>(),
+                            t[4].cast<double>(), t[5].cast<double>()});
+            py::gil_scoped_release nogil;
+            return warpdb::ResidentShards::synthetic(n_rows, sc, devices);
+          },
+          py::arg("n_rows"), py::arg("columns"), py::arg("devices") = 0,
+          "n_rows generated in HBM over `devices` GPUs; columns = [(name, DataType, seed, kind, lo, hi)]")
+      .def_property_readonly("num_rows", &warpdb::ResidentShards::num_rows)
+      .def_property_readonly("num_shards", &warpdb::ResidentShards::num_shards)
+      .def("ranges",
+           [](const warpdb::ResidentShards &r) {
+             py::list out;
+             for (auto &s : r.ranges()) out.append(py::make_tuple(s.device, s.begin, s.end));
+             return out;
+           })
+      .def("sum", &warpdb::ResidentShards::sum, py::arg("expr"), py::arg("cond") = "",
+           py::call_guard<py::gil_scoped_release>())
+      .def(
+          "group_sum",
+          [](const warpdb::ResidentShards &r, const std::string &val, const std::string &key, const std::string &cond,
+             int32_t key_lo) {
+            warpdb::GroupResult g;
+            {
+              py::gil_scoped_release nogil;
+              g = r.group_sum(val, key, cond, key_lo);
+            }
+            return group_arrays(g);
+          },
+          py::arg("val"), py::arg("key"), py::arg("cond") = "", py::arg("key_window_lo") = 0)
+      .def("dense", &warpdb::ResidentShards::dense, py::arg("expr"), py::arg("cond") = "",
+           py::call_guard<py::gil_scoped_release>());
 
   m.def(
       "analyze_condition",

@@ -200,20 +200,54 @@ void WarpDB::query_arrow_device(const std::string &expr, ArrowDeviceArray *out_a
   export_device_to_arrow(static_cast<float *>(out.release()), n, dev, out_array, out_schema);
 }
 
-std::vector<float> WarpDB::query_multi_gpu(const std::string &expr) {
+// The row shards of query_multi_gpu*, built on first use.  With one visible
+// GPU holding table_ the shard IS table_ (borrowed, no second HBM copy).
+warpdb::ResidentShards &WarpDB::shards() {
   if (host_table_.num_rows() == 0) throw std::runtime_error("Host table not available for multi-GPU query");
+  if (!shards_) {
+    int ndev = 0;
+    hip_ok(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    if (ndev == 1 && table_.device == 0)
+      shards_ = warpdb::ResidentShards::borrow(table_);
+    else
+      shards_ = std::make_unique<warpdb::ResidentShards>(host_table_);
+  }
+  return *shards_;
+}
+
+std::vector<float> WarpDB::query_multi_gpu(const std::string &expr) {
   std::string e, c;
   lower_query(expr, names_of(host_table_), e, c);
-  if (!shards_) shards_ = std::make_unique<warpdb::ResidentShards>(host_table_);
-  return shards_->dense(e, c);
+  return shards().dense(e, c);
 }
 
 std::pair<double, int64_t> WarpDB::query_multi_gpu_sum(const std::string &expr) {
-  if (host_table_.num_rows() == 0) throw std::runtime_error("Host table not available for multi-GPU query");
   std::string e, c;
   lower_query(expr, names_of(host_table_), e, c);
-  if (!shards_) shards_ = std::make_unique<warpdb::ResidentShards>(host_table_);
-  return shards_->sum(e, c);
+  return shards().sum(e, c);
+}
+
+warpdb::GroupResult WarpDB::query_multi_gpu_group(const std::string &sql, int32_t key_window_lo) {
+  QueryAST ast;
+  try {
+    ast = parse_query(tokenize(sql));
+  } catch (const std::exception &e) {
+    throw std::runtime_error(std::string("Failed to parse SQL: ") + e.what());
+  }
+  const auto cols = names_of(host_table_);
+  auto *agg = ast.select_list.empty() ? nullptr : dynamic_cast<const AggregationNode *>(ast.select_list[0].get());
+  if (!ast.group_by || !agg) throw std::runtime_error("query_multi_gpu_group expects SELECT <agg>(expr) ... GROUP BY key");
+  if (ast.group_by->keys.size() != 1) throw std::runtime_error("GROUP BY supports one key expression");
+  if (!ast.joins.empty()) throw std::runtime_error("JOIN is not supported by the execution engine");
+  validate_ast(agg->expr.get(), cols);
+  validate_ast(ast.group_by->keys[0].get(), cols);
+  std::string cond;
+  if (ast.where) {
+    validate_ast(ast.where->get(), cols);
+    cond = (*ast.where)->to_cuda_expr();
+  }
+  // SUM / COUNT / AVG all derive from the (sum, count) the shards exchange
+  return shards().group_sum(agg->expr->to_cuda_expr(), ast.group_by->keys[0]->to_cuda_expr(), cond, key_window_lo);
 }
 
 std::vector<float> WarpDB::query_multi_gpu_csv(const std::string &csv_path, const std::string &expr,
