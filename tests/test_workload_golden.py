@@ -1,0 +1,160 @@
+"""Parity at workload scale, pinned to the reference's own output.
+
+tests/golden/workload_*.npz hold what the reference's CPU path computed
+(oracle/_ref/ref_harness, i.e. the reference's load_csv_to_host / eval_node
+compiled from /root/reference) on 100 000-row synthetic tables of the
+BASELINE.json shapes; tests/golden/make_workload_golden.py made them.
+
+CPU tests: the table regenerated here hashes to the CSV the reference read,
+and the oracle (oracle/warpdb_oracle.c) equals the reference's result.
+GPU tests: the HIP path through the C ABI equals the reference's result
+directly -- compaction indices and float bits, GROUP BY keys / counts / double
+sums, top-K rows and keys.
+"""
+from __future__ import annotations
+
+import hashlib
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib as ora
+import synth
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+sys.path.insert(0, GOLDEN)
+import make_workload_golden as mk  # noqa: E402  (generator + CSV formatting of the fixtures)
+
+with open(os.path.join(GOLDEN, "workload_golden.json")) as _f:
+    META = json.load(_f)
+N = META["rows"]
+
+
+def table(name):
+    if name in ("c2", "c4"):
+        return synth.c2_table(N), ()
+    if name == "c3":
+        return synth.c3_table(N), ("quantity",)
+    return mk.c5_table(N), ()
+
+
+def fixture(name):
+    return np.load(os.path.join(GOLDEN, f"workload_{name}.npz"))
+
+
+def compaction_fixture(name):
+    f = fixture(name)
+    idx = np.nonzero(np.unpackbits(f["mask"])[:N])[0].astype(np.int64)
+    return idx, f["bits"]
+
+
+@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5"])
+def test_regenerated_table_is_the_reference_input(name):
+    cols, ints = table(name)
+    text = mk.csv_text(cols, ints)
+    assert hashlib.sha256(text.encode()).hexdigest() == META["cases"][name]["csv_sha256"]
+
+
+@pytest.mark.parametrize("name", ["c2", "c4"])
+def test_oracle_equals_reference_compaction(name):
+    cols, _ = table(name)
+    e, c = ora.split_where(META["cases"][name]["query"])
+    vals, idx = ora.project_filter(ora.HostTable(cols), e, c, sem=ora.SEM_CPU)
+    ridx, rbits = compaction_fixture(name)
+    assert len(ridx) == META["cases"][name]["passing"]
+    assert np.array_equal(idx, ridx)
+    assert np.array_equal(vals.view(np.uint32), rbits)
+
+
+def test_oracle_equals_reference_group_by():
+    cols, _ = table("c3")
+    k, s, c = ora.group_sum(ora.HostTable(cols), "price", "quantity", sem=ora.SEM_CPU)
+    f = fixture("c3")
+    assert np.array_equal(k, f["keys"]) and np.array_equal(c, f["counts"])
+    assert np.array_equal(s, f["sums"])  # double sums of float values: exact here
+
+
+def test_oracle_equals_reference_topk():
+    cols, _ = table("c5")
+    keys, idx, _ = ora.topk(ora.HostTable(cols), "price", 32, True)
+    f = fixture("c5")
+    assert np.array_equal(idx, f["rows"]) and np.array_equal(keys.view(np.uint32), f["bits"])
+
+
+# ---------------------------------------------------------------- GPU
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["c2", "c4"])
+@pytest.mark.parametrize("idx_bytes", [4, 8])
+def test_hip_compaction_equals_reference(name, idx_bytes):
+    torch = pytest.importorskip("torch")
+    from test_gpu_parity import dev_table, gpu_compact
+
+    cols, _ = table(name)
+    t, _ = dev_table(cols)
+    e, c = ora.split_where(META["cases"][name]["query"])
+    vals, idx = gpu_compact(t, ora.lower(e), ora.lower(c), idx_bytes=idx_bytes)
+    ridx, rbits = compaction_fixture(name)
+    assert np.array_equal(idx.astype(np.int64), ridx)
+    assert np.array_equal(vals.view(np.uint32), rbits)
+    del torch
+
+
+@pytest.mark.gpu
+def test_hip_dense_equals_reference():
+    torch = pytest.importorskip("torch")
+    from test_gpu_parity import dev_table, launch
+    from warpdb_amd import _warpexec as wx
+
+    cols, _ = table("c2")
+    t, _ = dev_table(cols)
+    out = torch.full((N,), float("nan"), dtype=torch.float32, device="cuda")
+    wx.project_filter(t, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", launch(), wx.MODE_DENSE_FILL,
+                      out.data_ptr(), 0, 4, 0)
+    ridx, rbits = compaction_fixture("c2")
+    o = out.cpu().numpy()
+    assert np.array_equal(o[ridx].view(np.uint32), rbits)
+    rest = np.ones(N, bool)
+    rest[ridx] = False
+    assert np.all(o[rest] == 0.0)
+
+
+@pytest.mark.gpu
+def test_hip_group_by_equals_reference():
+    torch = pytest.importorskip("torch")
+    from test_gpu_parity import dev_table, launch
+    from warpdb_amd import _warpexec as wx
+
+    cols, _ = table("c3")
+    t, _ = dev_table(cols)
+    cap = 4096
+    keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+    sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+    g = wx.group_sum(t, "price[idx]", "quantity[idx]", None, launch(), 0, cap, keys.data_ptr(), sums.data_ptr(),
+                     cnts.data_ptr())
+    f = fixture("c3")
+    assert g == len(f["keys"])
+    assert np.array_equal(keys[:g].cpu().numpy(), f["keys"]) and np.array_equal(cnts[:g].cpu().numpy(), f["counts"])
+    assert np.array_equal(sums[:g].cpu().numpy(), f["sums"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k", [5, 32])
+def test_hip_topk_equals_reference(k):
+    torch = pytest.importorskip("torch")
+    from test_gpu_parity import dev_table, launch
+    from warpdb_amd import _warpexec as wx
+
+    cols, _ = table("c5")
+    t, _ = dev_table(cols)
+    tk = torch.empty(k, dtype=torch.float32, device="cuda")
+    ti = torch.empty(k, dtype=torch.int64, device="cuda")
+    m = wx.topk(t, "price[idx]", None, None, k, True, launch(), tk.data_ptr(), ti.data_ptr(), 0)
+    f = fixture("c5")
+    assert m == k
+    assert np.array_equal(ti.cpu().numpy(), f["rows"][:k])
+    assert np.array_equal(tk.cpu().numpy().view(np.uint32), f["bits"][:k])

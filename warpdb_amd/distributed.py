@@ -320,10 +320,27 @@ class ShardedQuery:
         return ok[:n].clone(), osm[:n].clone(), oc[:n].clone()
 
     # --- top-K ------------------------------------------------------------
-    def topk(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int, descending: bool):
+    def topk_device(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int,
+                    descending: bool):
+        """This shard's top-K (keys, global rows, SELECT values, count) on the
+        device, asynchronous; ties by ascending row index, NaN last."""
         tk = self._buf("tk", k, torch.float32)
         ti = self._buf("ti", k, torch.int64)
         tv = self._buf("tv", k, torch.float32)
-        m = self.wx.topk(self.table, order_expr, cond, select_expr, k, descending, self.launch_sync, tk.data_ptr(),
-                         ti.data_ptr(), tv.data_ptr(), row_base=self.shard.row_base)
+        tn = self._buf("tn", 1, torch.int64)
+        self.wx.topk(self.table, order_expr, cond, select_expr, k, descending, self.launch, tk.data_ptr(),
+                     ti.data_ptr(), tv.data_ptr(), row_base=self.shard.row_base, d_count=tn.data_ptr(),
+                     want_count=False)
+        return tk, ti, tv, tn
+
+    def topk(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int, descending: bool):
+        """Global top-K as host tensors: one all-gather of every shard's K
+        candidates, then the (key, row) merge; a single shard is already final."""
+        tk, ti, tv, tn = self.topk_device(order_expr, cond, select_expr, k, descending)
+        if self.world == 1:
+            m = int(tn.item())  # synchronises
+            self.wx.check(self.launch)
+            return tk[:m].cpu(), ti[:m].cpu(), tv[:m].cpu()
+        m = int(tn.item())
+        self.wx.check(self.launch)
         return merge_topk(tk, ti, tv, m, k, descending, self.group)
