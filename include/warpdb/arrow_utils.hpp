@@ -15,3 +15,14 @@ void export_to_arrow(const float *data, int64_t length, bool use_shared_memory, 
 // device_type ARROW_DEVICE_ROCM.  Ownership of d_data passes to the array:
 // its release() calls hipFree.
 void export_device_to_arrow(float *d_data, int64_t length, int device, ArrowDeviceArray *out, ArrowSchema *schema);
+
+// The compacted result (passing rows only, ascending row order) as an Arrow
+// struct<value: float32, row: int64> array named "result"; host buffers are
+// copied into malloc'd memory that release() frees.
+void export_compact_to_arrow(const float *values, const int64_t *rows, int64_t length, ArrowArray *out_array,
+                             ArrowSchema *out_schema);
+
+// Zero-copy device export of a compacted result (ARROW_DEVICE_ROCM):
+// ownership of both device buffers passes to the array (release() hipFrees them).
+void export_device_compact_to_arrow(float *d_values, int64_t *d_rows, int64_t length, int device,
+                                    ArrowDeviceArray *out, ArrowSchema *schema);

@@ -55,6 +55,10 @@ class WarpDB {
   warpdb::GroupResult query_multi_gpu_group(const std::string &sql, int32_t key_window_lo = 0);
   // Zero-copy result: dense device buffer as an ArrowDeviceArray (ROCm).
   void query_arrow_device(const std::string &expr, ArrowDeviceArray *out_array, ArrowSchema *out_schema);
+  // The compacted result (passing rows only) as struct<value: float32, row: int64>:
+  // host copy, and zero-copy in HBM (ARROW_DEVICE_ROCM; buffers sized for n_rows).
+  void query_arrow_compact(const std::string &expr, ArrowArray *out_array, ArrowSchema *out_schema);
+  void query_arrow_device_compact(const std::string &expr, ArrowDeviceArray *out_array, ArrowSchema *out_schema);
 
   const Table &table() const { return table_; }
   const HostTable &host_table() const { return host_table_; }

@@ -47,6 +47,40 @@ py::tuple group_arrays(const warpdb::GroupResult &g) {
                         py::array_t<int64_t>(static_cast<py::ssize_t>(g.counts.size()), g.counts.data()));
 }
 
+py::tuple device_capsules(ArrowDeviceArray *arr, ArrowSchema *schema) {
+  // named as the Arrow PyCapsule interface names device arrays
+  py::capsule a(arr, "arrow_device_array", [](PyObject *o) {
+    auto *x = static_cast<ArrowDeviceArray *>(PyCapsule_GetPointer(o, "arrow_device_array"));
+    if (x) {
+      if (x->array.release) x->array.release(&x->array);
+      delete x;
+    }
+  });
+  py::capsule s(schema, "arrow_schema", [](PyObject *o) {
+    auto *x = static_cast<ArrowSchema *>(PyCapsule_GetPointer(o, "arrow_schema"));
+    if (x) {
+      if (x->release) x->release(x);
+      delete x;
+    }
+  });
+  return py::make_tuple(a, s);
+}
+
+template <typename Arr, typename F>
+py::tuple export_with(F &&fn, py::tuple (*wrap)(Arr *, ArrowSchema *)) {
+  auto *arr = new Arr();
+  auto *schema = new ArrowSchema();
+  try {
+    py::gil_scoped_release nogil;
+    fn(arr, schema);
+  } catch (...) {
+    delete arr;
+    delete schema;
+    throw;
+  }
+  return wrap(arr, schema);
+}
+
 py::tuple arrow_capsules(ArrowArray *arr, ArrowSchema *schema) {
   py::capsule a(arr, [](void *p) {
     auto *x = static_cast<ArrowArray *>(p);
@@ -98,6 +132,29 @@ PYBIND11_MODULE(pywarpdb, m) {
           },
           py::arg("expr"), py::arg("shared_memory") = false,
           "Return result as Arrow C Data Interface capsules (ArrowArray, ArrowSchema).")
+      .def(
+          "query_arrow_device",
+          [](WarpDB &db, const std::string &expr) {
+            return export_with<ArrowDeviceArray>(
+                [&](ArrowDeviceArray *a, ArrowSchema *s) { db.query_arrow_device(expr, a, s); }, device_capsules);
+          },
+          py::arg("expr"),
+          "Dense result left in HBM: (ArrowDeviceArray capsule, ArrowSchema capsule), device_type ARROW_DEVICE_ROCM.")
+      .def(
+          "query_arrow_compact",
+          [](WarpDB &db, const std::string &expr) {
+            return export_with<ArrowArray>([&](ArrowArray *a, ArrowSchema *s) { db.query_arrow_compact(expr, a, s); },
+                                           arrow_capsules);
+          },
+          py::arg("expr"), "Passing rows as struct<value: float32, row: int64> (Arrow C Data Interface capsules).")
+      .def(
+          "query_arrow_device_compact",
+          [](WarpDB &db, const std::string &expr) {
+            return export_with<ArrowDeviceArray>(
+                [&](ArrowDeviceArray *a, ArrowSchema *s) { db.query_arrow_device_compact(expr, a, s); },
+                device_capsules);
+          },
+          py::arg("expr"), "Passing rows as struct<value, row> in HBM (ArrowDeviceArray capsule, ROCm).")
       .def("query_compact", &WarpDB::query_compact, py::call_guard<py::gil_scoped_release>())
       .def("query_sum", &WarpDB::query_sum, py::call_guard<py::gil_scoped_release>())
       .def("query_multi_gpu_sum", &WarpDB::query_multi_gpu_sum, py::call_guard<py::gil_scoped_release>())

@@ -215,6 +215,32 @@ warpdb::ResidentShards &WarpDB::shards() {
   return *shards_;
 }
 
+void WarpDB::query_arrow_compact(const std::string &expr, ArrowArray *out_array, ArrowSchema *out_schema) {
+  auto r = query_compact(expr);
+  export_compact_to_arrow(r.first.data(), r.second.data(), static_cast<int64_t>(r.first.size()), out_array,
+                          out_schema);
+}
+
+void WarpDB::query_arrow_device_compact(const std::string &expr, ArrowDeviceArray *out_array,
+                                        ArrowSchema *out_schema) {
+  std::string e, c;
+  lower(expr, e, c);
+  const int64_t n = table_.num_rows;
+  // sized for every row passing; the array's length is the passing count
+  DeviceBuffer vals(table_.device, sizeof(float) * static_cast<size_t>(n ? n : 1));
+  DeviceBuffer rows(table_.device, sizeof(int64_t) * static_cast<size_t>(n ? n : 1));
+  WxTableView v(table_);
+  wx_launch L = sync_launch(table_.device);
+  int64_t count = 0;
+  char err[8192];
+  throw_on(wx_project_filter(&v.table, e.c_str(), c.c_str(), &L, WX_MODE_COMPACT, static_cast<float *>(vals.ptr),
+                             rows.ptr, 8, 0, nullptr, &count, err, sizeof(err)),
+           err);
+  const int dev = table_.device;
+  export_device_compact_to_arrow(static_cast<float *>(vals.release()), static_cast<int64_t *>(rows.release()), count,
+                                 dev, out_array, out_schema);
+}
+
 std::vector<float> WarpDB::query_multi_gpu(const std::string &expr) {
   std::string e, c;
   lower_query(expr, names_of(host_table_), e, c);
