@@ -65,6 +65,16 @@ VARIANTS = {
     "nolb_unaligned": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_DIAG_NO_LOOKBACK=2"},
     "deep_dw12": {"WARPDB_COMPACT_SCHED": "deep", "WARPDB_COMPACT_DWAVES": "12"},
     "deep_dw15_g3": {"WARPDB_COMPACT_SCHED": "deep", "WARPDB_COMPACT_GROUPS": "3"},
+    "deep_g2": {"WARPDB_COMPACT_GROUPS": "2"},
+    "ticket": {"WARPDB_COMPACT_SCHED": "ticket"},
+    "static": {"WARPDB_COMPACT_SCHED": "static"},
+    "deep_g3": {"WARPDB_COMPACT_GROUPS": "3"},
+    "deep_dw8": {"WARPDB_COMPACT_DWAVES": "8"},
+    "deep_dw8_g2": {"WARPDB_COMPACT_DWAVES": "8", "WARPDB_COMPACT_GROUPS": "2"},
+    "deep_dw6_2pc": {"WARPDB_COMPACT_DWAVES": "6", "WARPDB_COMPACT_BPC_FORCE": "2",
+                     "WARPDB_EXTRA_DEFINES": "WX_COMPACT_MINBLOCKS=2"},
+    "deep_dw5_g4_2pc": {"WARPDB_COMPACT_DWAVES": "5", "WARPDB_COMPACT_BPC_FORCE": "2",
+                        "WARPDB_EXTRA_DEFINES": "WX_COMPACT_MINBLOCKS=2"},
     "dw12": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_COMPACT_DWAVES": "12"},
     "lb_sleep0": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_LB_SLEEP=0"},
     "lb_sleep1": {"WARPDB_COMPACT_SCHED": "static", "WARPDB_EXTRA_DEFINES": "WX_LB_SLEEP=1"},

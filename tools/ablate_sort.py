@@ -42,6 +42,35 @@ VARIANTS = {
     "hcopies32": {D: "WX_RS_HCOPIES=32"},
     "hunroll2": {D: "WX_RS_HUNROLL=2"},
     "hunroll8": {D: "WX_RS_HUNROLL=8"},
+    "rank_base0": {D: "WX_RS_RANK_BASE=0"},
+    "items24_minw6": {D: "WX_RS_MINW=6", "WARPDB_RS_ITEMS": "24"},
+    "items28": {"WARPDB_RS_ITEMS": "28"},
+    "items32": {"WARPDB_RS_ITEMS": "32"},
+    "items12_minw6": {D: "WX_RS_MINW=6", "WARPDB_RS_ITEMS": "12"},
+    "items20": {"WARPDB_RS_ITEMS": "20"},
+    "items34": {"WARPDB_RS_ITEMS": "34"},
+    "items36": {"WARPDB_RS_ITEMS": "36"},
+    "items40": {"WARPDB_RS_ITEMS": "40"},
+    "items48": {"WARPDB_RS_ITEMS": "48"},
+    "b1024_i16": {"WARPDB_RS_BLOCK": "1024", "WARPDB_RS_ITEMS": "16"},
+    "b1024_i20": {"WARPDB_RS_BLOCK": "1024", "WARPDB_RS_ITEMS": "20"},
+    "b768_i20": {"WARPDB_RS_BLOCK": "768", "WARPDB_RS_ITEMS": "20"},
+    "b384_i40": {"WARPDB_RS_BLOCK": "384", "WARPDB_RS_ITEMS": "40"},
+    "b256_i48": {"WARPDB_RS_BLOCK": "256", "WARPDB_RS_ITEMS": "48"},
+    "items32_lbw2": {"WARPDB_RS_ITEMS": "32", "WARPDB_RS_LBW": "2"},
+    "lbw4": {"WARPDB_RS_LBW": "4"},
+    "nosplit": {D: "WX_RS_SPLIT=0"},
+    "b256_i32": {"WARPDB_RS_BLOCK": "256", "WARPDB_RS_ITEMS": "32", D: "WX_RS_SPLIT=0"},
+    "b256_i32_split": {"WARPDB_RS_BLOCK": "256", "WARPDB_RS_ITEMS": "32"},
+    "b256_i28": {"WARPDB_RS_BLOCK": "256", "WARPDB_RS_ITEMS": "28", D: "WX_RS_SPLIT=0"},
+    "b320_i32": {"WARPDB_RS_BLOCK": "320", "WARPDB_RS_ITEMS": "32", D: "WX_RS_SPLIT=0"},
+    "b384_i28": {"WARPDB_RS_BLOCK": "384", "WARPDB_RS_ITEMS": "28", D: "WX_RS_SPLIT=0"},
+    "b448_i24": {"WARPDB_RS_BLOCK": "448", "WARPDB_RS_ITEMS": "24", D: "WX_RS_SPLIT=0"},
+    "nosplit_lbw2": {D: "WX_RS_SPLIT=0", "WARPDB_RS_LBW": "2"},
+    "lbw8": {"WARPDB_RS_LBW": "8"},
+    "lbw4_first": {"WARPDB_RS_LBW": "4", D: "WX_RS_LB_FIRST=1"},
+    "lbw4_i28": {"WARPDB_RS_LBW": "4", "WARPDB_RS_ITEMS": "28"},
+    "items32_g1": {"WARPDB_RS_ITEMS": "32", D: "WX_RS_RANK_G=1"},
 }
 KNOBS = (D, "WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW")
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 10**9

@@ -19,6 +19,7 @@ if len(sys.argv) > 2:
 t = wx.Table(1 << 20, [wx.Column("price", wx.FLOAT32, 1 << 20), wx.Column("quantity", wx.FLOAT32, 2 << 20)])
 t_int = wx.Table(1 << 20, [wx.Column("price", wx.FLOAT32, 1 << 20), wx.Column("quantity", wx.INT32, 2 << 20)])
 jobs = {
+    "dense": (t, wx.OP_DENSE, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", None, 0),
     "compact": (t, wx.OP_COMPACT, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", None, 0),
     "sum": (t, wx.OP_SUM, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", None, 0),
     "group": (t_int, wx.OP_GROUP, "price[idx]", None, "quantity[idx]", 0),

@@ -44,7 +44,7 @@ typedef unsigned int wx_u32;
 #define WX_RS_BLOCK 512  // >= 256: threads 0..255 own one digit each
 #endif
 #ifndef WX_RS_ITEMS
-#define WX_RS_ITEMS 20
+#define WX_RS_ITEMS 32
 #endif
 #define WX_RS_TILE (WX_RS_BLOCK * WX_RS_ITEMS)
 #define WX_RS_EPOCHS 63

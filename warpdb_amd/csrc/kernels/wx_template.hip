@@ -243,16 +243,131 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 // WX_BLOCK * WX_UNROLL row quads per iteration and issues all their loads
 // first; each quad's four results leave as one 16-byte store when the quad
 // is full (fill, or every row passing) and as guarded dword stores otherwise.
-// 8 quads per thread, 2 workgroups per CU, nontemporal stores: 2.20 ms per
-// 1e9 rows with fill (12 B/row, 5.45 TB/s), against 2.20-2.34 ms for plain
-// stores across grids and unrolls (profiles/r01/ablate_dense.txt).  Without
-// fill every partially selected 64-B line is a masked write: 3.1 ms.
+// Nontemporal stores: 2.20 ms per 1e9 rows with fill (12 B/row, 5.45 TB/s),
+// against 2.20-2.34 ms for plain stores across grids and unrolls
+// (profiles/r01/ablate_dense.txt).  The software-pipelined loop below (4
+// quads per thread, 3 workgroups per CU) takes 2.12 ms against 2.165 for the
+// best unpipelined geometry (profiles/r02/abl_dense_*.txt).  Without fill
+// every partially selected 64-B line is a masked write: 3.1 ms.
 #ifndef WX_UNROLL
-#define WX_UNROLL 8
+#define WX_UNROLL 4
 #endif
 #ifndef WX_DENSE_NT_STORE
 #define WX_DENSE_NT_STORE 1
 #endif
+#ifndef WX_DENSE_PIPE
+#define WX_DENSE_PIPE 1
+#endif
+// One span's rows: evaluate and store (full spans: one 16-byte store per quad).
+#define WX_DENSE_SPAN_OUT(FULL)                                                                        \
+  _Pragma("unroll") for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {                                   \
+    const wx_i64 wx_r0 = WX_QUAD(wx_u) << 2;                                                           \
+    if (WX_QUAD(wx_u) >= wx_nq) continue;                                                              \
+    float wx_o[4];                                                                                     \
+    bool wx_k[4];                                                                                      \
+    _Pragma("unroll") for (int wx_e = 0; wx_e < 4; ++wx_e) {                                          \
+      WX_COLS(WX_BIND_U)                                                                               \
+      const wx_i64 idx = wx_r0 + wx_e;                                                                 \
+      (void)idx;                                                                                       \
+      wx_k[wx_e] = WX_EVAL_COND();                                                                     \
+      wx_o[wx_e] = static_cast<float>(WX_EXPR);                                                        \
+    }                                                                                                  \
+    const bool wx_all = wx_k[0] && wx_k[1] && wx_k[2] && wx_k[3];                                      \
+    if ((FULL) && (wx_a.fill || wx_all)) {                                                             \
+      f4 v;                                                                                            \
+      v.x = wx_k[0] ? wx_o[0] : 0.0f;                                                                  \
+      v.y = wx_k[1] ? wx_o[1] : 0.0f;                                                                  \
+      v.z = wx_k[2] ? wx_o[2] : 0.0f;                                                                  \
+      v.w = wx_k[3] ? wx_o[3] : 0.0f;                                                                  \
+      ::wx::st_sel<WX_DENSE_NT_STORE>(reinterpret_cast<f4 *>(wx_a.out + wx_r0), v);                   \
+    } else {                                                                                           \
+      _Pragma("unroll") for (int wx_e = 0; wx_e < 4; ++wx_e) if (wx_r0 + wx_e < wx_a.n_rows &&        \
+                                                                  (wx_k[wx_e] || wx_a.fill))           \
+          wx_a.out[wx_r0 + wx_e] = wx_k[wx_e] ? wx_o[wx_e] : 0.0f;                                    \
+    }                                                                                                  \
+  }
+#if WX_DENSE_PIPE
+// Software-pipelined steady state: while this span and the next are whole
+// and every row is written (fill, or no WHERE), the next span's loads are
+// issued before this span's stores and waited for after them.  On gfx9
+// stores count in vmcnt, so the straight-line body lets the wait leave this
+// span's stores in flight (a conditional store or load anywhere in the loop
+// makes the compiler drain vmcnt to 0).  Ragged spans and masked output take
+// the generic loop below.
+#define WX_DECL_N(name, T, slot) T wx_n##slot[WX_UNROLL][4];
+#define WX_LOAD_N_FAST(name, T, slot) ::wx::load4_full<T>(wx_a.col[slot], wx_r0u, wx_n##slot[wx_u]);
+#define WX_MOVE_N(name, T, slot)                                  \
+  _Pragma("unroll") for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) \
+      _Pragma("unroll") for (int wx_e = 0; wx_e < 4; ++wx_e) wx_u##slot[wx_u][wx_e] = wx_n##slot[wx_u][wx_e];
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseArgs wx_a) {
+  typedef float f4 __attribute__((ext_vector_type(4)));
+  const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
+  const wx_i64 wx_nfull = wx_a.n_rows >> 2;
+  const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_SPAN;
+  wx_i64 wx_base = (wx_i64)blockIdx.x * WX_SPAN;
+  const bool wx_every = wx_a.fill || !WX_HAS_COND;
+  if (WX_ALIGNED16 && wx_every && wx_base + WX_SPAN <= wx_nfull) {
+    WX_COLS(WX_DECL_U)
+    WX_COLS(WX_DECL_N)
+#pragma unroll
+    for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+      const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;
+      WX_COLS(WX_LOAD_N_FAST)
+    }
+    // Drain here, so the loop head inherits no pending loads: otherwise the
+    // wait the compiler places there for this prologue (vmcnt(0)) also
+    // drains every later iteration's stores.
+    __builtin_amdgcn_s_waitcnt(0x0f70);  // gfx9: vmcnt(0) expcnt(7) lgkmcnt(15)
+    WX_COLS(WX_MOVE_N)
+    while (true) {
+      const wx_i64 wx_nb = wx_base + wx_stride;
+      const bool wx_more = wx_nb + WX_SPAN <= wx_nfull;  // workgroup-uniform
+      if (wx_more) {
+#pragma unroll
+        for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+          const wx_i64 wx_r0u = (wx_nb + (wx_i64)wx_u * WX_BLOCK + threadIdx.x) << 2;
+          WX_COLS(WX_LOAD_N_FAST)
+        }
+      }
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+        const wx_i64 wx_r0 = WX_QUAD(wx_u) << 2;
+        f4 v;
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e) {
+          WX_COLS(WX_BIND_U)
+          const wx_i64 idx = wx_r0 + wx_e;
+          (void)idx;
+          const bool wx_k = WX_EVAL_COND();
+          v[wx_e] = wx_k ? static_cast<float>(WX_EXPR) : 0.0f;
+        }
+        ::wx::st_sel<WX_DENSE_NT_STORE>(reinterpret_cast<f4 *>(wx_a.out + wx_r0), v);
+      }
+      wx_base = wx_nb;
+      if (!wx_more) break;
+      WX_COLS(WX_MOVE_N)
+    }
+  }
+  for (; wx_base < wx_nq; wx_base += wx_stride) {
+    WX_COLS(WX_DECL_U)
+    const bool wx_full = WX_ALIGNED16 && wx_base + WX_SPAN <= wx_nfull;
+    if (wx_full) {
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+        const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;
+        WX_COLS(WX_LOAD_U_FAST)
+      }
+    } else {
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+        const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;
+        WX_COLS(WX_LOAD_U)
+      }
+    }
+    WX_DENSE_SPAN_OUT(wx_full)
+  }
+}
+#else
 extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseArgs wx_a) {
   typedef float f4 __attribute__((ext_vector_type(4)));
   const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
@@ -308,6 +423,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
     }
   }
 }
+#endif  // WX_DENSE_PIPE
 #endif
 
 // ===========================================================================
@@ -1919,7 +2035,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApply
 // and the abort word, and the launch drains.
 #define WX_RS_WAVES (WX_RS_BLOCK / 64)
 #ifndef WX_RS_LBW
-#define WX_RS_LBW 1  // predecessor words per digit per look-back round (8 measured slower: poll traffic)
+#define WX_RS_LBW 2  // predecessor words per digit per look-back round (keys: 2 by 0.1-0.2 ms over 1; 8 slower)
 #endif
 #ifndef WX_STALL_TICKS
 #define WX_STALL_TICKS 200000000ull  // 2 s at 100 MHz without progress (see the compaction look-back)
@@ -2033,6 +2149,9 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_i_d(WxRadix
 #ifndef WX_RS_DIAG_NO_STORE
 #define WX_RS_DIAG_NO_STORE 0  // diagnostic: keys are read out of LDS but not written (results invalid)
 #endif
+#ifndef WX_RS_RANK_BASE
+#define WX_RS_RANK_BASE 1  // counts by plain LDS read + lowest-lane store (no returning atomic, no broadcast)
+#endif
 #ifndef WX_RS_MATCH_LDS
 // Digit peers of a key by one ds_or_b64 of the lane's bit into a per-digit
 // LDS mask (then read back and cleared): 3 LDS operations per key instead of
@@ -2109,13 +2228,18 @@ __device__ __forceinline__ void wx_rs_rank(const WxRadixPassArgs &a, WxRsShared 
     // one ballot and stay off LDS: a few-valued digit (the exponent byte)
     // would otherwise send most of the wave's ORs to one word, serialized.
     bool lds[G];
+    wx_u32 d0[G];  // lane 0's digit of item g (wave-uniform)
+    wx_u64 lm[G];  // the lanes sharing it
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       lds[g] = valid[g];
+      d0[g] = 0u;
+      lm[g] = 0ull;
       if (WX_RS_RANK_LEAD) {
-        const wx_u32 d0 = __builtin_amdgcn_readfirstlane(d[g]);  // lane 0 (valid if any lane is)
-        const bool lead = valid[g] && d[g] == d0;
-        m[g] = __builtin_amdgcn_ballot_w64(lead);
+        d0[g] = __builtin_amdgcn_readfirstlane(d[g]);  // lane 0 (valid if any lane is)
+        const bool lead = valid[g] && d[g] == d0[g];
+        lm[g] = __builtin_amdgcn_ballot_w64(lead);
+        m[g] = lm[g];
         lds[g] = valid[g] && !lead;
       }
     }
@@ -2126,10 +2250,51 @@ __device__ __forceinline__ void wx_rs_rank(const WxRadixPassArgs &a, WxRsShared 
     for (int g = 0; g < G; ++g)
       if (lds[g]) m[g] = __hip_atomic_load(w[g], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
       else if (!valid[g]) m[g] = 0ull;
+#if WX_RS_RANK_BASE
+    // Counts without a returning atomic: every key reads its digit's running
+    // count (base) together with its peer mask, and the group's lowest lane
+    // stores base + group size back.  One dependent LDS round trip per round
+    // instead of three (mask read -> leader's atomic add -> broadcast).  Item
+    // g > 0 also counts the earlier items' keys of its digit in this round:
+    // their mask words are still set (cleared below), and the lanes of lane
+    // 0's digit group, which stayed off LDS, are known from the ballot.
+    wx_u32 base[G], before[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      base[g] = 0u;
+      before[g] = 0u;
+      if (valid[g]) {
+        base[g] = __hip_atomic_load(&S.wc[wave][d[g]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#pragma unroll
+        for (int h = 0; h < g; ++h) {
+          const wx_u64 mh = __hip_atomic_load(peers + ((h * WX_RS_WAVES + wave) * 256 + d[g]), __ATOMIC_RELAXED,
+                                              __HIP_MEMORY_SCOPE_WAVEFRONT);
+          before[g] += (wx_u32)__builtin_popcountll(mh) +
+                       ((WX_RS_RANK_LEAD && d[g] == d0[h]) ? (wx_u32)__builtin_popcountll(lm[h]) : 0u);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      rk[i + g] = 0u;
+      if (valid[g]) {
+        const wx_u32 b = base[g] + before[g];
+        rk[i + g] = b + (wx_u32)__builtin_popcountll(m[g] & below);
+        if ((m[g] & below) == 0ull)  // the group's lowest lane; item g's store follows item g - 1's
+          __hip_atomic_store(&S.wc[wave][d[g]], b + (wx_u32)__builtin_popcountll(m[g]), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WAVEFRONT);
+      }
+    }
+#endif
     __builtin_amdgcn_wave_barrier();
 #pragma unroll
     for (int g = 0; g < G; ++g)
       if (lds[g]) __hip_atomic_store(w[g], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WAVEFRONT);
+#if WX_RS_RANK_BASE
+    __builtin_amdgcn_wave_barrier();
+    continue;
+#endif
 #else
 #pragma unroll
     for (int g = 0; g < G; ++g) {
@@ -2250,6 +2415,110 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
   }
 }
 
+#ifndef WX_RS_SPLIT
+// 1: the keys (and payloads) are permuted into LDS by their tile-local
+// slots, which need only this tile's counts, before the look-back resolves
+// the tile's global offsets: the permutation overlaps the look-back's first
+// poll instead of waiting behind the whole look-back.  Key + payload tiles:
+// 19.8 vs 21.8 ms per 1e9 pairs; keys alone lose the extra barrier's worth
+// (15.4 vs 14.9 ms), so only the pair module sets it (abl_sort_split.txt).
+#define WX_RS_SPLIT 0
+#endif
+// Split form, part 1 (every thread; holds a barrier): threads 0..255 own
+// digit tid, publish its count {A} (or {P} for tile 0), then the exclusive
+// prefix over the waves (S.wc) and over the digits (S.ld).  Returns the
+// tile's count of digit tid.
+__device__ __forceinline__ wx_u32 wx_rs_local(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const wx_u64 E = (wx_u64)a.epoch << 58;
+  const bool look = tile != 0 && !WX_RS_DIAG_NO_LOOKBACK;
+  wx_u32 tot = 0u, inc = 0u;
+  if (tid < 256) {
+#pragma unroll
+    for (int w = 0; w < WX_RS_WAVES; ++w) {
+      const wx_u32 c = S.wc[w][tid];
+      S.wc[w][tid] = tot;
+      tot += c;
+    }
+    wx::st_agent(&a.status[(wx_u64)tile * 256 + tid], E | (look ? WX_RS_FLAG_A : WX_RS_FLAG_P) | tot);
+    inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_u32 t = __shfl_up(inc, o);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) S.wsum[wave] = inc;
+  }
+  __syncthreads();
+  if (tid < 256) {
+    wx_u32 ld = inc - tot;
+    for (int w = 0; w < wave; ++w) ld += S.wsum[w];
+    S.ld[tid] = ld;
+  }
+  return tot;
+}
+
+// Split form, part 2 (threads 0..255): look back over the preceding tiles'
+// words of digit tid to an inclusive {P} (`first` is predecessor tile - 1's
+// word, loaded earlier), publish {P}, set S.gb.
+__device__ __forceinline__ void wx_rs_resolve(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile, wx_u32 tot,
+                                              wx_u64 first) {
+  const int tid = threadIdx.x;
+  const wx_u64 E = (wx_u64)a.epoch << 58;
+  const bool look = tile != 0 && !WX_RS_DIAG_NO_LOOKBACK;
+  wx_u64 excl = 0;
+  if (look) {
+    wx_i64 p = (wx_i64)tile - 1;
+    wx_u32 spins = 0;
+    wx_u64 t_last = 0ull;
+    bool fresh = true;
+    while (true) {
+      wx_u64 wv[WX_RS_LBW];
+#pragma unroll
+      for (int j = 0; j < WX_RS_LBW; ++j)
+        wv[j] = (j == 0 && fresh) ? first
+                : p - j >= 0    ? wx::ld_agent(&a.status[(wx_u64)(p - j) * 256 + tid])
+                                : (E | WX_RS_FLAG_P);
+      fresh = false;
+      int stop = WX_RS_LBW;
+      bool done = false;
+#pragma unroll
+      for (int j = 0; j < WX_RS_LBW; ++j) {
+        if (stop == WX_RS_LBW && !done) {
+          const wx_u64 flag = (wv[j] >> 56) & 3ull;
+          if ((wv[j] >> 58) != (wx_u64)a.epoch || flag == 0ull) {
+            stop = j;
+          } else {
+            excl += wv[j] & WX_RS_VAL_MASK;
+            done = flag == 2ull;
+          }
+        }
+      }
+      if (done) break;
+      if (stop == WX_RS_LBW) {
+        p -= WX_RS_LBW;
+        t_last = 0ull;
+        continue;
+      }
+      if (stop > 0) t_last = 0ull;
+      p -= stop;
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 63u) == 0u) {
+        const wx_u64 now = __builtin_amdgcn_s_memrealtime();
+        if (t_last == 0ull) {
+          t_last = now;
+        } else if (now - t_last > WX_STALL_TICKS) {
+          atomicOr(a.err, WX_DEVERR_LOOKBACK);
+          atomicExch(&a.ctl[1], 1u);
+        }
+        if (__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+      }
+    }
+    wx::st_agent(&a.status[(wx_u64)tile * 256 + tid], E | WX_RS_FLAG_P | (excl + tot));
+  }
+  S.gb[tid] = a.digit_base[tid] + (wx_u32)excl - S.ld[tid];
+}
+
 // Keys into digit order in LDS; pos[i] keeps each key's tile-local slot
 // (the payload follows through the same slots).
 template <int KIND, bool ASC>
@@ -2330,9 +2599,19 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
   wx_rs_load<PAY>(a, wb, tb + WX_RS_TILE <= a.n, x, v);
   wx_rs_rank<KIND, ASC>(a, S, peers, wb, x, rk);
   __syncthreads();
-  wx_rs_digits(a, S, tile);
-  __syncthreads();
-  wx_rs_scatter<KIND, ASC>(a, S, wb, x, rk, pos, s_k);
+  if (WX_RS_SPLIT) {
+    const wx_u32 tot = wx_rs_local(a, S, tile);
+    __syncthreads();  // S.ld
+    wx_u64 first = 0ull;
+    if (tid < 256 && tile != 0 && !WX_RS_DIAG_NO_LOOKBACK)
+      first = wx::ld_agent(&a.status[(wx_u64)(tile - 1) * 256 + tid]);  // in flight during the permutation
+    wx_rs_scatter<KIND, ASC>(a, S, wb, x, rk, pos, s_k);
+    if (tid < 256) wx_rs_resolve(a, S, tile, tot, first);
+  } else {
+    wx_rs_digits(a, S, tile);
+    __syncthreads();
+    wx_rs_scatter<KIND, ASC>(a, S, wb, x, rk, pos, s_k);
+  }
   __syncthreads();
   wx_rs_store<KIND, ASC>(a, S, tile_n, s_k, gdst);
   if (PAY) wx_rs_payload(a, tile_n, wb, v, pos, gdst, s_k);
