@@ -78,6 +78,7 @@ def parse():
     p.add_argument("--cpu-sample", type=float, default=5e7, help="rows for the CPU baseline sample")
     p.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU run (0: all)")
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-check", action="store_true", help="skip the post-timing result check")
     return p.parse_args()
 
 
@@ -225,6 +226,104 @@ def pmc_traffic(workload, n):
     return None
 
 
+# ------------------------------------------------- result check
+CHECK_CHUNK = 1 << 28  # rows per torch pass of the check (bounds its temporaries)
+
+
+def self_check(workload, sq, cols, n, world, wd, torch, out_v=None):
+    """One more query after the timed steps, its exchanged result checked
+    against torch on each rank's shard (all-reduced): counts and row ids
+    exact, float values bit for bit, double sums to 1e-12 relative.  Raises
+    (no JSON line) on a mismatch; returns a short description."""
+    price = cols["price"]
+    _, expr, aux, _ = WORKLOADS[workload]
+
+    def red(x, op=torch.distributed.ReduceOp.SUM if world > 1 else None):
+        t = torch.as_tensor(x, dtype=torch.float64, device="cuda").reshape(-1).clone()
+        return wd.all_reduce_(t, op=op) if world > 1 else t
+
+    def chunks():
+        for c0 in range(0, n, CHECK_CHUNK):
+            yield c0, min(n, c0 + CHECK_CHUNK)
+
+    if workload == "project":
+        vals, idx, off, total = sq.compact(expr, aux, idx_bytes=8)
+        qty = cols["quantity"]
+        pos, seen = 0, 0
+        for c0, c1 in chunks():
+            m = price[c0:c1] > 15.0
+            rows = torch.nonzero(m).reshape(-1) + (c0 + sq.shard.row_base)
+            k = rows.numel()
+            if not torch.equal(idx[pos:pos + k], rows):
+                raise SystemExit(f"check failed: compaction row ids differ in rows [{c0}, {c1})")
+            want = (price[c0:c1] * qty[c0:c1])[m]
+            if not torch.equal(vals[pos:pos + k].view(torch.int32), want.view(torch.int32)):
+                raise SystemExit(f"check failed: compaction values differ in rows [{c0}, {c1})")
+            pos += k
+            seen += k
+        if seen != vals.numel() or int(red(seen)[0]) != total:
+            raise SystemExit(f"check failed: passing count {vals.numel()} / {total} vs {seen}")
+        return f"ok: {total} passing rows, ids and value bits equal torch on every shard"
+    if workload == "dense":
+        qty = cols["quantity"]
+        for c0, c1 in chunks():
+            p_, q_ = price[c0:c1], qty[c0:c1]
+            want = torch.where(p_ > 15.0, p_ * q_, torch.zeros_like(p_))
+            if not torch.equal(out_v[c0:c1].view(torch.int32), want.view(torch.int32)):
+                raise SystemExit(f"check failed: dense output differs in rows [{c0}, {c1})")
+        return "ok: dense output bits equal torch"
+    if workload == "sort":
+        for c0, c1 in chunks():
+            a = out_v[c0:min(n, c1 + 1)]
+            if not bool((a[1:] >= a[:-1]).all()):
+                raise SystemExit(f"check failed: not sorted in [{c0}, {c1})")
+        sums = red([price.double().sum().item(), out_v[:n].double().sum().item()])
+        if abs(float(sums[0]) - float(sums[1])) > 1e-12 * abs(float(sums[0])):
+            raise SystemExit("check failed: the sorted values are not a permutation of the input")
+        return "ok: ascending, same sum as the input"
+    if workload == "sum":
+        got_s, got_c = sq.sum(expr, aux)
+        acc = [0.0, 0]
+        for c0, c1 in chunks():
+            p_ = price[c0:c1]
+            m = p_ > 20.0
+            acc[0] += (p_ * 0.9)[m].double().sum().item()
+            acc[1] += int(m.sum().item())
+        want = red(acc)
+        if got_c != int(want[1]) or abs(got_s - float(want[0])) > 1e-12 * abs(float(want[0])):
+            raise SystemExit(f"check failed: SUM {got_s} / {got_c} vs {float(want[0])} / {int(want[1])}")
+        return f"ok: count {got_c} exact, sum {got_s:.6e} within 1e-12"
+    if workload == "group":
+        keys, sums, counts = sq.group_sum(expr, aux, None, 0, 4096)
+        key = cols["quantity"]
+        ws = torch.zeros(1024, dtype=torch.float64, device="cuda")
+        wc = torch.zeros(1024, dtype=torch.float64, device="cuda")
+        for c0, c1 in chunks():
+            kk = key[c0:c1].long()
+            ws.index_add_(0, kk, price[c0:c1].double())
+            wc += torch.bincount(kk, minlength=1024).double()
+        ws, wc = red(ws), red(wc)
+        present = torch.nonzero(wc).reshape(-1)
+        if not torch.equal(keys.long(), present) or not torch.equal(counts, wc[present].long()):
+            raise SystemExit("check failed: GROUP BY keys / counts differ from torch")
+        if not bool(((sums - ws[present]).abs() <= 1e-12 * ws[present].abs()).all()):
+            raise SystemExit("check failed: GROUP BY sums differ from torch beyond 1e-12")
+        return f"ok: {keys.numel()} groups, keys and counts exact, sums within 1e-12"
+    if workload == "topk":
+        tk, ti, tv = sq.topk(expr, None, aux, 5, True)
+        cand = torch.cat([torch.topk(price[c0:c1], min(5, c1 - c0)).values for c0, c1 in chunks()] +
+                         [torch.full((5,), float("-inf"), device="cuda")])
+        cand = torch.topk(cand, 5).values  # this shard's 5 best (padded), equal sizes for the all-gather
+        cand = wd.all_gather(cand) if world > 1 else cand
+        want = torch.topk(cand.float(), 5).values.cpu()
+        if not torch.equal(tk.view(torch.int32), want.view(torch.int32)):
+            raise SystemExit(f"check failed: top-5 keys {tk.tolist()} vs {want.tolist()}")
+        if not torch.equal(tv.view(torch.int32), (tk * 0.9).view(torch.int32)):
+            raise SystemExit("check failed: discount(price, 0.9) values differ")
+        return "ok: top-5 keys and discount() values bit-equal torch"
+    return None
+
+
 # ------------------------------------------------- one process per GPU
 def main_ranks(args):
     import torch
@@ -324,6 +423,8 @@ def main_ranks(args):
 
     # algorithmic bytes per launch of the dominant kernel
     passing = int(counts.item()) if workload == "project" else None
+    check = None if args.no_check else self_check(workload, sq, cols, n, world, wd, torch,
+                                                  out_v if workload in ("dense", "sort") else None)
     rb = READ_BYTES[workload]
     if workload == "project":
         bytes_per_launch = n * 8 + passing * 8  # 4 B value + 4 B int32 index per passing row
@@ -348,6 +449,7 @@ def main_ranks(args):
                           "parallelism": f"row-sharded x{world}, one process per GPU"}
         if passing is not None:
             line["config"]["passing_rows_per_gpu"] = passing
+        line["check"] = check
         line["roofline"] = roofline(bytes_per_launch, kern_avg_ms, n * rb, kname, pmc_traffic(workload, n),
                                     "HIP events around the dominant kernel on its stream (max over ranks)")
         line["cpu_baseline"] = cpu_leg(args, workload) if world == 1 else None

@@ -297,3 +297,5 @@ def test_bench_json_contract(args):
         assert key in line, key
     assert line["value"] > 0 and line["roofline"]["achieved"] > 0 and line["roofline"]["frac"] < 1.0
     assert line["scaling"] == ("strong" if "--total-rows" in args else "weak")
+    if "--api" not in args:  # the bench's own post-timing check of the exchanged result
+        assert str(line["check"]).startswith("ok"), line["check"]

@@ -242,9 +242,16 @@ def test_sharded_query_single_rank():
     dist.destroy_process_group()
 
 
-def test_bench_two_ranks_on_one_gpu():
-    # the multi-rank bench path (torchrun rendezvous, shards, exchanges, max-over-
-    # ranks timing) with two ranks sharing the GPU over gloo; RCCL on the 8-GPU node
+@pytest.mark.parametrize("workload,extra", [
+    ("project", ["--rows", "1e7"]),
+    ("sum", ["--total-rows", "20000001"]),  # C4's strong-scaling form, ragged shards
+    ("group", ["--rows", "5e6"]),           # the dense-window all-reduce
+    ("topk", ["--rows", "5e6"]),
+])
+def test_bench_two_ranks_on_one_gpu(workload, extra):
+    # the multi-rank bench path (torchrun rendezvous, shards, the product's
+    # exchanges, max-over-ranks timing) with two ranks sharing the GPU over
+    # gloo; RCCL on the 8-GPU node
     import json
     import socket
     import sys
@@ -255,11 +262,17 @@ def test_bench_two_ranks_on_one_gpu():
     env = dict(os.environ, WARPDB_DIST_BACKEND="gloo")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
-                        "--gpus", "2", "--rows", "1e7", "--steps", "3", "--warmup", "1"],
+                        "--gpus", "2", "--workload", workload, "--steps", "3", "--warmup", "1", *extra],
                        capture_output=True, text=True, cwd=ROOT, env=env, timeout=600)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     lines = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
     assert len(lines) == 1
     d = lines[0]
-    assert d["n_gpus"] == 2 and d["config"]["total_rows"] == 2 * 10**7 and d["value"] > 0
-    assert d["config"]["passing_rows_per_gpu"] > 0.6 * 10**7
+    assert d["n_gpus"] == 2 and d["value"] > 0 and d["cpu_baseline"] is None
+    assert str(d["check"]).startswith("ok"), d["check"]
+    if workload == "project":
+        assert d["config"]["total_rows"] == 2 * 10**7 and d["scaling"] == "weak"
+        assert d["config"]["passing_rows_per_gpu"] > 0.6 * 10**7
+    if workload == "sum":
+        assert d["config"]["total_rows"] == 20000001 and d["scaling"] == "strong"
+        assert d["config"]["rows_per_gpu"] == 10000001
