@@ -14,7 +14,7 @@ warpdb_amd.distributed.ShardedQuery, with the exchange each result needs
   project  all-gather of the per-shard passing counts (global placement)
   sum      all-reduce of {sum, count} as two doubles          (C4)
   group    all-reduce of the 4097-double key window            (C3)
-  topk     all-gather of K packed candidates + merge           (C5)
+  topk     all-gather of K packed candidates + merge on the device (C5)
   dense    none (WarpDB::query's dense contract, src/warpdb.cpp:243-256)
   sort     single GPU only (ORDER BY without LIMIT: projection + radix sort)
 
@@ -396,8 +396,8 @@ def main_ranks(args):
         def step():
             sq.group_sum_device(expr, aux, None, 0, 4096)
     else:
-        def step():
-            sq.topk(expr, None, aux, 5, True)
+        def step():  # results stay in HBM like the other workloads' (no host round trip per query)
+            sq.topk_merged_device(expr, None, aux, 5, True)
 
     for _ in range(args.warmup):
         step()

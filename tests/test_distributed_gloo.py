@@ -117,6 +117,17 @@ def _worker(rank: int, world: int, port: int, n: int, errq):
             full = {"p": np.floor(synth.uniform_f32(n, 1, 0, 40)).astype(np.float32)}
             rk2, ri2, _ = ora.topk(ora.HostTable(full), "p", 5, desc)
             assert np.array_equal(mk.numpy(), rk2) and np.array_equal(mi.numpy(), ri2)
+            # the device-side merge (no host round trip): k slots per shard,
+            # unused ones filled with junk and masked by the shard's count
+            m = len(tk)
+            pk = torch.full((5,), float("nan")); pi = torch.full((5,), -7, dtype=torch.int64)
+            pv = torch.full((5,), 123.0)
+            pk[:m] = torch.from_numpy(tk); pi[:m] = torch.from_numpy(ti + b); pv[:m] = torch.from_numpy(tv)
+            dk, di, dv, dn = wd.merge_topk_device(pk, pi, pv, torch.tensor([m]), 5, desc)
+            c = int(dn[0])
+            assert c == len(rk2)
+            assert np.array_equal(dk[:c].numpy().view(np.uint32), mk.numpy().view(np.uint32))
+            assert np.array_equal(di[:c].numpy(), mi.numpy()) and np.array_equal(dv[:c].numpy(), mv.numpy())
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as ex:  # report to the parent

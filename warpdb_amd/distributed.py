@@ -16,7 +16,8 @@ the C ABI.  The exchanges are the ones the result needs, one collective each
                shard saw keys outside the window, an all-gather merge of
                those groups follows
   top-K        all-gather of K packed candidates (key, value, row) + count
-               per shard, merged by (key, row)
+               per shard, merged by (key, row) -- on the host (merge_topk) or,
+               without a host round trip, on the device (merge_topk_device)
 
 With the "nccl" backend these run on RCCL over xGMI on device tensors; with
 "gloo" (CPU tests, or several ranks sharing one GPU) the same code stages
@@ -198,6 +199,38 @@ def merge_topk(keys: torch.Tensor, idx: torch.Tensor, vals: torch.Tensor, n: int
     return merge_topk_candidates(gk, gi, gv, k, descending)
 
 
+def merge_topk_device(keys: torch.Tensor, idx: torch.Tensor, vals: torch.Tensor, count: torch.Tensor, k: int,
+                      descending: bool, group=None):
+    """merge_topk without a host round trip: one all-gather of every shard's
+    k candidate slots (unused slots masked by the shard's device-side count),
+    then stable sorts on the device -- by row, by key, by class (number,
+    NaN, unused slot) -- so ties keep the smallest row and NaN sorts last.
+    Returns (keys, rows, vals) of k slots and the global count min(k, total),
+    all on the device of `keys` (gloo stages through the host)."""
+    dev = keys.device
+    if _single(group):
+        return keys[:k], idx[:k].to(torch.int64), vals[:k], torch.clamp(count.reshape(1).to(torch.int64), max=k)
+    rec = torch.zeros(2 * k + 1, dtype=torch.int64, device=dev)
+    rec[0:1] = count.reshape(1).to(torch.int64)
+    rec[1: 1 + 2 * k: 2] = (_f32_bits(keys[:k]) << 32) | _f32_bits(vals[:k])
+    rec[2: 2 + 2 * k: 2] = idx[:k].to(torch.int64)
+    allr = all_gather(rec, group).view(-1, 2 * k + 1)
+    n = allr[:, 0:1]
+    body = allr[:, 1:].reshape(-1, k, 2)
+    kv, gi = body[:, :, 0].reshape(-1), body[:, :, 1].reshape(-1)
+    gk = ((kv >> 32) & 0xFFFFFFFF).to(torch.int32).view(torch.float32)
+    gv = (kv & 0xFFFFFFFF).to(torch.int32).view(torch.float32)
+    used = (torch.arange(k, device=dev).reshape(1, k) < n).reshape(-1)
+    cls = torch.where(used, torch.isnan(gk).to(torch.int64), torch.full_like(gi, 2))
+    fill = float("-inf") if descending else float("inf")
+    key = torch.where(cls == 0, gk, torch.full_like(gk, fill))
+    order = torch.argsort(gi, stable=True)
+    order = order[torch.argsort(key[order], descending=descending, stable=True)]
+    order = order[torch.argsort(cls[order], stable=True)][:k]
+    total = torch.clamp(n.sum().reshape(1), max=k)
+    return gk[order], gi[order], gv[order], total
+
+
 @dataclass
 class Shard:
     """This rank's slice of a row-sharded table, resident on its GPU."""
@@ -332,6 +365,13 @@ class ShardedQuery:
                      ti.data_ptr(), tv.data_ptr(), row_base=self.shard.row_base, d_count=tn.data_ptr(),
                      want_count=False)
         return tk, ti, tv, tn
+
+    def topk_merged_device(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int,
+                           descending: bool):
+        """Global top-K left in HBM, no host synchronisation: this shard's
+        candidates, then merge_topk_device.  Returns (keys, rows, vals, count)."""
+        tk, ti, tv, tn = self.topk_device(order_expr, cond, select_expr, k, descending)
+        return merge_topk_device(tk, ti, tv, tn, k, descending, self.group)
 
     def topk(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int, descending: bool):
         """Global top-K as host tensors: one all-gather of every shard's K
