@@ -318,7 +318,8 @@ class ShardedQuery:
         the 4097-double window, the final merge on the device.  Returns
         (keys, sums, counts, n_groups) device tensors of `capacity` entries;
         reads one double back to learn whether any shard saw keys outside
-        the window (then their groups are all-gathered and merged)."""
+        the window (then their groups are all-gathered and merged).  With a
+        single shard it is wx_group_sum alone (asynchronous)."""
         wx = self.wx
         window = self._buf("gwin", GROUP_EXCHANGE_DOUBLES, torch.float64)[:GROUP_EXCHANGE_DOUBLES]
         xk = self._buf("gxk", capacity, torch.int32)
@@ -329,6 +330,10 @@ class ShardedQuery:
         osm = self._buf("gos", capacity, torch.float64)
         oc = self._buf("goc", capacity, torch.int64)
         ng = self._buf("gng", 1, torch.int64)
+        if self.world == 1:  # one shard: the single-GPU kernel + finalize, nothing to exchange or read back
+            wx.group_sum(self.table, val_expr, key_expr, cond, self.launch, key_lo, capacity, ok.data_ptr(),
+                         osm.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr(), want_count=False)
+            return ok, osm, oc, ng
         wx.group_partials(self.table, val_expr, key_expr, cond, self.launch, key_lo, window.data_ptr(), capacity,
                           xk.data_ptr(), xs.data_ptr(), xc.data_ptr(), d_n_extra=nx.data_ptr())
         exchange_group_window(window, self.group)
