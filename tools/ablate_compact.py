@@ -67,6 +67,7 @@ VARIANTS = {
     "deep_dw15_g3": {"WARPDB_COMPACT_SCHED": "deep", "WARPDB_COMPACT_GROUPS": "3"},
     "deep_g2": {"WARPDB_COMPACT_GROUPS": "2"},
     "ticket": {"WARPDB_COMPACT_SCHED": "ticket"},
+    "deep_retire_acqrel": {"WARPDB_EXTRA_DEFINES": "WX_RETIRE_ACQ_REL=1"},
     "static": {"WARPDB_COMPACT_SCHED": "static"},
     "deep_g3": {"WARPDB_COMPACT_GROUPS": "3"},
     "deep_dw8": {"WARPDB_COMPACT_DWAVES": "8"},

@@ -571,11 +571,22 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
 // The last workgroup of a compaction launch to retire returns the tile
 // ticket to 0 for the next launch on this workspace (no host memset per
 // query).  Every workgroup calls it once after its last ticket fetch.
+// Relaxed is enough: every ticket fetch of a workgroup has RETURNED (its
+// value went through LDS and a barrier) before that workgroup's increment
+// is issued, the increments are ordered on their one address, so the reset
+// follows every fetch of the launch; the next launch sees it across the
+// kernel boundary.  (acq_rel here is a buffer_wbl2 + buffer_inv at agent
+// scope, a few µs at the end of every launch.)
+#ifndef WX_RETIRE_ACQ_REL
+#define WX_RETIRE_ACQ_REL 0
+#endif
 __device__ __forceinline__ void wx_retire(wx_u64 *ctrs) {
-  const wx_u64 done = __hip_atomic_fetch_add(&ctrs[2], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+  const wx_u64 done = WX_RETIRE_ACQ_REL
+                          ? __hip_atomic_fetch_add(&ctrs[2], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
+                          : __hip_atomic_fetch_add(&ctrs[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (done == (wx_u64)gridDim.x - 1ull) {
     __hip_atomic_store(&ctrs[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(&ctrs[2], 0ull, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(&ctrs[2], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
