@@ -534,7 +534,9 @@ def _sort_input(n, seed):
 
 
 # the bitonic path is a cross-check at small sizes only
-@pytest.mark.parametrize("sort,n", [("radix", n) for n in (8191, 10240, 10241, 24577, 3_000_017)]
+# radix tile edges: key tiles hold 512 x 32 = 16 384 keys, key + payload tiles 512 x 20 = 10 240
+@pytest.mark.parametrize("sort,n", [("radix", n) for n in (8191, 10240, 10241, 16383, 16384, 16385, 24577,
+                                                           3 * 16384 + 1, 3_000_017)]
                          + [("bitonic", 8191)])
 def test_sort_float_stable_nan_signed_zero(n, sort, monkeypatch):
     monkeypatch.setenv("WARPDB_SORT", sort)
@@ -546,7 +548,7 @@ def test_sort_float_stable_nan_signed_zero(n, sort, monkeypatch):
         assert np.array_equal(bits(t.cpu().numpy()), bits(ref))
 
 
-@pytest.mark.parametrize("n", [12288, 12289, 100_003, 2_500_001])
+@pytest.mark.parametrize("n", [10240, 10241, 12288, 12289, 2 * 10240 + 1, 100_003, 2_500_001])
 @pytest.mark.parametrize("span", ["narrow", "full"])
 def test_sort_pairs_radix_stable(n, span):
     # narrow keys leave three digits constant (those passes are skipped);
