@@ -37,6 +37,14 @@ struct GroupResult {
   std::vector<int64_t> counts;
 };
 
+// ORDER BY key [DESC] LIMIT k over every shard: the winning order keys, their
+// global row numbers and the SELECT values, best first (ties by row).
+struct TopkResult {
+  std::vector<float> keys;
+  std::vector<int64_t> rows;
+  std::vector<float> values;
+};
+
 // One synthetic column (wx_fill_synthetic's counter-based generator, so each
 // device generates its own rows at their global row numbers).
 struct SyntheticColumn {
@@ -75,6 +83,10 @@ class ResidentShards {
   // combine through one RCCL all-reduce of the dense window, others by a host merge
   GroupResult group_sum(const std::string &val_cuda, const std::string &key_cuda, const std::string &cond_cuda,
                         int32_t key_lo = 0) const;
+  // ORDER BY order [DESC] LIMIT k (1..32) WHERE cond, SELECT select (empty: the
+  // order key): K candidates per shard, ONE RCCL all-gather, a merge on the host
+  TopkResult topk(const std::string &order_cuda, const std::string &cond_cuda, const std::string &select_cuda, int k,
+                  bool descending) const;
 
  private:
   ResidentShards();

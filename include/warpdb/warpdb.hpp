@@ -53,6 +53,10 @@ class WarpDB {
   // [key_window_lo, key_window_lo + 2048) merged on the host).  Groups in
   // ascending key order with double sums and counts (SUM / COUNT / AVG).
   warpdb::GroupResult query_multi_gpu_group(const std::string &sql, int32_t key_window_lo = 0);
+  // "SELECT e FROM t [WHERE c] ORDER BY o [ASC|DESC] LIMIT k" (k <= 32) over
+  // every GPU: K candidates per GPU, one RCCL all-gather, the (key, row) merge.
+  // The winning ORDER BY keys, global row numbers and SELECT values, best first.
+  warpdb::TopkResult query_multi_gpu_topk(const std::string &sql);
   // Zero-copy result: dense device buffer as an ArrowDeviceArray (ROCm).
   void query_arrow_device(const std::string &expr, ArrowDeviceArray *out_array, ArrowSchema *out_schema);
   // The compacted result (passing rows only) as struct<value: float32, row: int64>:

@@ -8,7 +8,7 @@
 * Compaction status epochs: more than 63 launches on one workspace (epoch
   wrap), shrinking / growing tables, every result bit-exact.
 * warpdb_amd.distributed.ShardedQuery without a process group (1 GPU) and
-  the C++ ResidentShards (synthetic shards, sum / group_sum) on every
+  the C++ ResidentShards (synthetic shards, sum / group_sum / topk) on every
   visible device, against the oracle.
 * Two host threads on one WarpDB (workspace lock).
 * bench.py end to end at small sizes for every workload (JSON contract).
@@ -229,6 +229,11 @@ def test_resident_shards_synthetic_sum_and_group(devices):
         rk, rsum, rcnt = ora.group_sum(ora.HostTable(host), "price", "quantity")
         assert np.array_equal(k, rk) and np.array_equal(cn, rcnt)
         np.testing.assert_allclose(sm, rsum, rtol=1e-12, atol=0)
+    # ORDER BY .. LIMIT k: K candidates per shard, one all-gather, the merge
+    for k, desc in ((5, True), (32, False), (1, True)):
+        tk, ti, tv = rs_.topk("price[idx]", "(quantity[idx] < 700)", "(price[idx] * 0.9f)", k, desc)
+        ok_, oi, ov = ora.topk(ora.HostTable(host), "price", k, desc, cond="quantity < 700", select_expr="price * 0.9")
+        assert np.array_equal(ti, oi) and np.array_equal(bits(tk), bits(ok_)) and np.array_equal(bits(tv), bits(ov))
 
 
 def test_warpdb_multi_gpu_group_and_shared_table():
@@ -243,6 +248,13 @@ def test_warpdb_multi_gpu_group_and_shared_table():
     assert db.query_multi_gpu_sum("price * 0.9 WHERE price > 20") == pytest.approx((27.0, 1))
     r = db.query_multi_gpu("price * quantity WHERE price > 10")
     assert list(r) == [31.5, 80.0, 30.5, 150.0]
+    # tests/sql_features_test.cpp:24-34: ORDER BY price DESC LIMIT 2 -> [30, 20]; OFFSET 1 LIMIT 2 -> [20, 15.25]
+    k, rows, v = db.query_multi_gpu_topk("SELECT price FROM test ORDER BY price DESC LIMIT 2")
+    assert v.tolist() == [30.0, 20.0] and rows.tolist() == [3, 1] and k.tolist() == [30.0, 20.0]
+    k, rows, v = db.query_multi_gpu_topk("SELECT price * quantity FROM test ORDER BY price DESC LIMIT 2 OFFSET 1")
+    assert k.tolist() == [20.0, 15.25] and rows.tolist() == [1, 2] and v.tolist() == [80.0, 30.5]
+    with pytest.raises(RuntimeError):
+        db.query_multi_gpu_topk("SELECT price FROM test ORDER BY price DESC LIMIT 40")
 
 
 def test_two_threads_share_one_warpdb():

@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdio>
 #include <condition_variable>
 #include <cstring>
@@ -246,11 +247,20 @@ struct GroupScratch {
   DeviceBuffer win, xk, xs, xc, nx, ok, os, oc, ng;
 };
 
+// Per-shard top-K candidates and their all-gathered copies (k <= 32).
+struct TopkScratch {
+  DeviceBuffer cand, all;  // [keys f32 x 32 | vals f32 x 32 | rows i64 x 32 | count i64], x shards for `all`
+  int shards = 0;
+};
+constexpr size_t kTopkMax = 32;
+constexpr size_t kTopkRec = kTopkMax * 4 + kTopkMax * 4 + kTopkMax * 8 + 8;  // bytes per shard record
+
 struct ResidentShards::Impl {
   int64_t n = 0;
   std::vector<ShardRange> ranges;
   std::vector<Shard> shards;
   std::vector<GroupScratch> group;
+  std::vector<TopkScratch> topk;
   std::mutex mu;  // one query at a time per object (shared workspaces and scratch)
 };
 
@@ -312,6 +322,7 @@ ResidentShards::~ResidentShards() {
     DevGuard g(impl_->ranges[i].device);
     impl_->shards[i] = Shard();
     if (i < impl_->group.size()) impl_->group[i] = GroupScratch();
+    if (i < impl_->topk.size()) impl_->topk[i] = TopkScratch();
   }
 }
 
@@ -347,6 +358,100 @@ std::vector<float> ResidentShards::dense(const std::string &expr_cuda, const std
     throw_on(wx_check(&L, err, sizeof(err)), err);
   });
   return result;
+}
+
+// ORDER BY .. LIMIT k over the shards: wx_topk per device
+// (global row numbers via the shard's row base) into one packed record,
+// ONE ncclAllGather of the records (bytes), then the (key, row) merge of
+// the <= 32 x shards candidates on the host.
+TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string &cond_cuda,
+                                const std::string &select_cuda, int k, bool descending) const {
+  if (k < 1 || k > static_cast<int>(kTopkMax)) throw std::runtime_error("top-K supports 1 <= k <= 32");
+  std::lock_guard<std::mutex> lk(impl_->mu);
+  TopkResult res;
+  const auto &ranges = impl_->ranges;
+  const size_t ns = ranges.size();
+  if (ns == 0) return res;
+  if (impl_->topk.size() < ns) impl_->topk.resize(ns);
+  std::vector<hipStream_t> streams(ns, nullptr);
+  run_per_device(ranges, [&](size_t i, const ShardRange &r) {
+    streams[i] = device_stream(r.device);
+    TopkScratch &t = impl_->topk[i];
+    if (t.shards != static_cast<int>(ns)) {
+      t.cand = DeviceBuffer(r.device, kTopkRec);
+      t.all = DeviceBuffer(r.device, kTopkRec * ns);
+      t.shards = static_cast<int>(ns);
+    }
+    char *c = static_cast<char *>(t.cand.ptr);
+    WxTableView v(impl_->shards[i].table);
+    wx_launch L = sync_launch(r.device, streams[i]);
+    L.flags = 0;  // asynchronous until after the collective
+    char err[8192];
+    throw_on(wx_topk(&v.table, order_cuda.c_str(), cond_cuda.c_str(), select_cuda.empty() ? nullptr : select_cuda.c_str(),
+                     k, descending ? 1 : 0, &L, r.begin, reinterpret_cast<float *>(c),
+                     reinterpret_cast<int64_t *>(c + kTopkMax * 8), reinterpret_cast<float *>(c + kTopkMax * 4),
+                     reinterpret_cast<int64_t *>(c + kTopkMax * 16), nullptr, err, sizeof(err)),
+             err);
+  });
+  if (ns > 1) {
+    Comms &cm = comms_for(static_cast<int>(ns));
+    std::lock_guard<std::mutex> clk(cm.mu);
+    if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
+    for (size_t i = 0; i < ns; ++i) {
+      DevGuard g(ranges[i].device);
+      if (ncclAllGather(impl_->topk[i].cand.ptr, impl_->topk[i].all.ptr, kTopkRec, ncclUint8, cm.comms[i],
+                        streams[i]) != ncclSuccess) {
+        (void)ncclGroupEnd();
+        throw std::runtime_error("ncclAllGather failed");
+      }
+    }
+    if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("RCCL all-gather failed");
+  }
+  char err[1024];
+  for (size_t i = 0; i < ns; ++i) {
+    DevGuard dg(ranges[i].device);
+    hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
+    wx_launch L = sync_launch(ranges[i].device, streams[i]);
+    throw_on(wx_check(&L, err, sizeof(err)), err);
+  }
+  std::vector<char> h(kTopkRec * ns);
+  {
+    DevGuard dg(ranges[0].device);
+    const void *src = ns > 1 ? impl_->topk[0].all.ptr : impl_->topk[0].cand.ptr;
+    hip_ok(hipMemcpy(h.data(), src, h.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+  }
+  struct Cand {
+    float key, val;
+    int64_t row;
+  };
+  std::vector<Cand> cand;
+  for (size_t i = 0; i < ns; ++i) {
+    const char *rec = h.data() + i * kTopkRec;
+    int64_t m = 0;
+    std::memcpy(&m, rec + kTopkMax * 16, 8);
+    for (int64_t j = 0; j < m; ++j) {
+      Cand c;
+      std::memcpy(&c.key, rec + 4 * j, 4);
+      std::memcpy(&c.val, rec + kTopkMax * 4 + 4 * j, 4);
+      std::memcpy(&c.row, rec + kTopkMax * 8 + 8 * j, 8);
+      cand.push_back(c);
+    }
+  }
+  // better key first (NaN last either way, -0.0 == +0.0), then the smaller row
+  auto better = [descending](const Cand &a, const Cand &b) {
+    const bool na = std::isnan(a.key), nb = std::isnan(b.key);
+    if (na != nb) return nb;
+    if (!na && a.key != b.key) return descending ? a.key > b.key : a.key < b.key;
+    return a.row < b.row;
+  };
+  std::sort(cand.begin(), cand.end(), better);
+  if (cand.size() > static_cast<size_t>(k)) cand.resize(k);
+  for (const Cand &c : cand) {
+    res.keys.push_back(c.key);
+    res.rows.push_back(c.row);
+    res.values.push_back(c.val);
+  }
+  return res;
 }
 
 std::pair<double, int64_t> ResidentShards::sum(const std::string &expr_cuda, const std::string &cond_cuda) const {

@@ -47,6 +47,12 @@ py::tuple group_arrays(const warpdb::GroupResult &g) {
                         py::array_t<int64_t>(static_cast<py::ssize_t>(g.counts.size()), g.counts.data()));
 }
 
+py::tuple topk_arrays(const warpdb::TopkResult &t) {
+  return py::make_tuple(py::array_t<float>(static_cast<py::ssize_t>(t.keys.size()), t.keys.data()),
+                        py::array_t<int64_t>(static_cast<py::ssize_t>(t.rows.size()), t.rows.data()),
+                        py::array_t<float>(static_cast<py::ssize_t>(t.values.size()), t.values.data()));
+}
+
 py::tuple device_capsules(ArrowDeviceArray *arr, ArrowSchema *schema) {
   // named as the Arrow PyCapsule interface names device arrays
   py::capsule a(arr, "arrow_device_array", [](PyObject *o) {
@@ -171,6 +177,17 @@ PYBIND11_MODULE(pywarpdb, m) {
           py::arg("sql"), py::arg("key_window_lo") = 0,
           "GROUP BY over every GPU (one RCCL all-reduce of the key window) -> (keys, sums, counts).")
       .def(
+          "query_multi_gpu_topk",
+          [](WarpDB &db, const std::string &sql) {
+            warpdb::TopkResult t;
+            {
+              py::gil_scoped_release nogil;
+              t = db.query_multi_gpu_topk(sql);
+            }
+            return topk_arrays(t);
+          },
+          py::arg("sql"), "ORDER BY .. LIMIT k over every GPU (one RCCL all-gather) -> (keys, rows, values).")
+      .def(
           "column_stats",
           [](const WarpDB &db) {
             warpdb::StatsMap m;
@@ -244,6 +261,19 @@ PYBIND11_MODULE(pywarpdb, m) {
             return group_arrays(g);
           },
           py::arg("val"), py::arg("key"), py::arg("cond") = "", py::arg("key_window_lo") = 0)
+      .def(
+          "topk",
+          [](const warpdb::ResidentShards &r, const std::string &order, const std::string &cond,
+             const std::string &select, int k, bool descending) {
+            warpdb::TopkResult t;
+            {
+              py::gil_scoped_release nogil;
+              t = r.topk(order, cond, select, k, descending);
+            }
+            return topk_arrays(t);
+          },
+          py::arg("order"), py::arg("cond") = "", py::arg("select") = "", py::arg("k") = 5,
+          py::arg("descending") = true)
       .def("dense", &warpdb::ResidentShards::dense, py::arg("expr"), py::arg("cond") = "",
            py::call_guard<py::gil_scoped_release>());
 

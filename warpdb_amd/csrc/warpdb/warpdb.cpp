@@ -276,6 +276,39 @@ warpdb::GroupResult WarpDB::query_multi_gpu_group(const std::string &sql, int32_
   return shards().group_sum(agg->expr->to_cuda_expr(), ast.group_by->keys[0]->to_cuda_expr(), cond, key_window_lo);
 }
 
+warpdb::TopkResult WarpDB::query_multi_gpu_topk(const std::string &sql) {
+  QueryAST ast;
+  try {
+    ast = parse_query(tokenize(sql));
+  } catch (const std::exception &e) {
+    throw std::runtime_error(std::string("Failed to parse SQL: ") + e.what());
+  }
+  if (ast.select_list.size() != 1 || ast.group_by || ast.distinct || !ast.order_by || !ast.limit)
+    throw std::runtime_error("query_multi_gpu_topk expects SELECT expr FROM t [WHERE c] ORDER BY o [DESC] LIMIT k");
+  if (dynamic_cast<const AggregationNode *>(ast.select_list[0].get()))
+    throw std::runtime_error("query_multi_gpu_topk takes a plain SELECT expression");
+  if (!ast.joins.empty()) throw std::runtime_error("JOIN is not supported by the execution engine");
+  const int64_t off = ast.offset ? ast.offset->count : 0, lim = ast.limit->count;
+  if (off < 0 || lim < 0 || off + lim > 32) throw std::runtime_error("query_multi_gpu_topk supports OFFSET + LIMIT <= 32");
+  const auto cols = names_of(host_table_);
+  validate_ast(ast.select_list[0].get(), cols);
+  validate_ast(ast.order_by->expr.get(), cols);
+  std::string cond;
+  if (ast.where) {
+    validate_ast(ast.where->get(), cols);
+    cond = (*ast.where)->to_cuda_expr();
+  }
+  warpdb::TopkResult r;
+  if (off + lim == 0) return r;
+  r = shards().topk(ast.order_by->expr->to_cuda_expr(), cond, ast.select_list[0]->to_cuda_expr(),
+                    static_cast<int>(off + lim), !ast.order_by->ascending);
+  const size_t drop = std::min(r.keys.size(), static_cast<size_t>(off));  // OFFSET
+  r.keys.erase(r.keys.begin(), r.keys.begin() + drop);
+  r.rows.erase(r.rows.begin(), r.rows.begin() + drop);
+  r.values.erase(r.values.begin(), r.values.begin() + drop);
+  return r;
+}
+
 std::vector<float> WarpDB::query_multi_gpu_csv(const std::string &csv_path, const std::string &expr,
                                                int rows_per_chunk) {
   if (rows_per_chunk <= 0) throw std::runtime_error("rows_per_chunk must be positive");
