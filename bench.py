@@ -24,8 +24,8 @@ With --gpus N the driver runs one process per GPU under torchrun (RCCL).
 
 --api runs the single-process C++ path instead (pywarpdb.ResidentShards:
 one host thread and stream per device, ncclCommInitAll over devices
-0..N-1 -- WarpDB::query_multi_gpu_sum / query_multi_gpu_group), for sum and
-group; its per-step time includes the collective and the host read-back.
+0..N-1 -- WarpDB::query_multi_gpu_sum / _group / _topk), for sum, group and
+topk; its per-step time includes the collective and the host read-back.
 
 Prints ONE JSON line (rank 0).
 """
@@ -483,8 +483,14 @@ def main_api(args):
     from warpdb_amd import pywarpdb as pw
 
     workload = args.workload
-    if workload not in ("sum", "group"):
-        raise SystemExit("--api covers the C++ multi-GPU aggregates: --workload sum | group")
+    if workload not in ("sum", "group", "topk"):
+        raise SystemExit("--api covers the C++ multi-GPU paths: --workload sum | group | topk")
+    if workload == "topk":  # the C++ path reads the custom.cu hook from $WARPDB_CUSTOM_PATH (src/jit.cpp:65-73)
+        import tempfile
+        hook = os.path.join(tempfile.mkdtemp(prefix="warpdb_bench_"), "custom.cu")
+        with open(hook, "w") as f:
+            f.write(DISCOUNT_SRC)
+        os.environ["WARPDB_CUSTOM_PATH"] = hook
     if int(os.environ.get("WORLD_SIZE", "1")) > 1:
         raise SystemExit("--api is one process driving every GPU; do not launch it under torchrun")
     devs = args.gpus
@@ -497,9 +503,12 @@ def main_api(args):
     if workload == "sum":
         def step():
             return shards.sum(expr, aux)
-    else:
+    elif workload == "group":
         def step():
             return shards.group_sum(expr, aux, "", 0)
+    else:
+        def step():
+            return shards.topk(expr, "", aux, 5, True)
 
     for _ in range(args.warmup):
         step()
@@ -510,8 +519,9 @@ def main_api(args):
     n_max = max(e - b for _, b, e in shards.ranges())
     line = line_common(args, shards.num_shards, n_total, elapsed, workload)
     line["config"] = {"workload": f"{query} ({workload})", "rows_per_gpu": n_max, "total_rows": n_total,
-                      "api": "pywarpdb.ResidentShards (WarpDB::query_multi_gpu_sum / query_multi_gpu_group)",
-                      "exchange": "ncclAllReduce " + ("2 x f64" if workload == "sum" else "4097 x f64") +
+                      "api": "pywarpdb.ResidentShards (WarpDB::query_multi_gpu_sum / _group / _topk)",
+                      "exchange": {"sum": "ncclAllReduce 2 x f64", "group": "ncclAllReduce 4097 x f64",
+                                   "topk": "ncclAllGather 520 B per shard"}[workload] +
                                   " over ncclCommInitAll(devices 0..n-1)",
                       "parallelism": f"row-sharded x{shards.num_shards}, one process, one thread + stream per GPU"}
     # the C++ path has no per-kernel events: the whole step bounds the kernel
@@ -519,8 +529,31 @@ def main_api(args):
     rb = READ_BYTES[workload]
     line["roofline"] = roofline(n_max * rb, ms, n_max * rb, kname, pmc_traffic(workload, n_max),
                                 "whole step (kernel + all-reduce + host read-back): a lower bound on the kernel")
+    line["check"] = api_check(workload, step(), n_total)
     line["cpu_baseline"] = cpu_leg(args, workload) if shards.num_shards == 1 else None
     print(json.dumps(line), flush=True)
+
+
+def api_check(workload, res, n_total):
+    """Size-independent properties of the C++ path's result (its data lives
+    inside ResidentShards): the tests pin the values themselves."""
+    import numpy as np
+
+    if workload == "sum":
+        s, c = res
+        if not (0 < c <= n_total and s > 0):
+            raise SystemExit(f"check failed: SUM {s} / {c}")
+        return f"ok: count {c} of {n_total} rows, sum {s:.6e}"
+    if workload == "group":
+        k, s, c = res
+        if int(np.asarray(c).sum()) != n_total or not bool(np.all(np.diff(np.asarray(k)) > 0)):
+            raise SystemExit("check failed: GROUP BY counts do not add up to the rows, or keys not ascending")
+        return f"ok: {len(k)} groups, counts add up to {n_total}, keys ascending"
+    k, rows, v = (np.asarray(x) for x in res)
+    want = (k.astype(np.float32) * np.float32(0.9)).astype(np.float32)
+    if len(k) != 5 or not bool(np.all(np.diff(k) <= 0)) or not np.array_equal(v.view(np.uint32), want.view(np.uint32)):
+        raise SystemExit("check failed: top-K keys not descending or discount() values differ")
+    return "ok: 5 keys descending, discount() values bit-equal"
 
 
 def main():

@@ -297,7 +297,8 @@ def test_two_threads_share_one_warpdb():
 @pytest.mark.parametrize("args", [
     ["--workload", "project"], ["--workload", "sum", "--total-rows", "3000001"], ["--workload", "group"],
     ["--workload", "topk"], ["--workload", "dense"], ["--workload", "sort"],
-    ["--workload", "sum", "--api", "--total-rows", "3000001"], ["--workload", "group", "--api"]])
+    ["--workload", "sum", "--api", "--total-rows", "3000001"], ["--workload", "group", "--api"],
+    ["--workload", "topk", "--api"]])
 def test_bench_json_contract(args):
     cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--rows", "2000003", "--steps", "3", "--warmup", "1",
            "--no-cpu-baseline"] + args
