@@ -79,6 +79,8 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU run (0: all)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-check", action="store_true", help="skip the post-timing result check")
+    p.add_argument("--no-secondary", action="store_true",
+                   help="project only: skip the SUM / GROUP BY lines measured beside the headline")
     return p.parse_args()
 
 
@@ -415,29 +417,35 @@ def main_ranks(args):
         if verbose:
             print(f"[bench rank {rank}] {what} {time.strftime('%H:%M:%S')}", file=sys.stderr, flush=True)
 
+    def timed(step_fn):
+        """W warm-up steps, then exactly K steps between barrier + synchronize;
+        (elapsed s, average timed-kernel ms, launches), max over ranks."""
+        for _ in range(args.warmup):
+            step_fn()
+        wx.check(L)
+        wx.timing_read()  # discard the warm-up launches
+        mark("timed steps")
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            step_fn()
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        k_ms, nl = wx.timing_read()
+        wx.check(L)
+        k_avg = k_ms / max(1, nl)
+        if world > 1:
+            t = torch.tensor([el, k_avg], dtype=torch.float64, device="cuda")
+            wd.all_reduce_(t, op=dist.ReduceOp.MAX)
+            el, k_avg = float(t[0]), float(t[1])
+        return el, k_avg, nl
+
     mark("warm-up")
-    for _ in range(args.warmup):
-        step()
-    wx.check(L)
-    wx.timing_read()  # discard the warm-up launches
-    mark("timed steps")
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms, launches = wx.timing_read()
-    wx.check(L)
-    kern_avg_ms = kern_ms / max(1, launches)
-    if world > 1:
-        t = torch.tensor([elapsed, kern_avg_ms], dtype=torch.float64, device="cuda")
-        wd.all_reduce_(t, op=dist.ReduceOp.MAX)
-        elapsed, kern_avg_ms = float(t[0]), float(t[1])
+    elapsed, kern_avg_ms, launches = timed(step)
 
     # algorithmic bytes per launch of the dominant kernel (DESIGN.md 5)
     passing = int(counts.item()) if workload == "project" else None
@@ -471,6 +479,37 @@ def main_ranks(args):
         line["check"] = check
         line["roofline"] = roofline(bytes_per_launch, kern_avg_ms, n * rb, kname, pmc_traffic(workload, n),
                                     "HIP events around the dominant kernel on its stream (max over ranks)")
+    # The other north-star aggregates on the same shards, timed the same way
+    # (so the driver's 1/2/4/8-GPU runs also measure SUM -- C4's 8e9 rows at
+    # 8 GPUs -- and GROUP BY scaling); reported beside the headline, not in it.
+    secondary = {}
+    if workload == "project" and not args.no_secondary:
+        qk = torch.empty(max(1, n), dtype=torch.int32, device="cuda")[:n]
+        wx.fill_synthetic(qk.data_ptr(), wx.INT32, n, 3, 1, 0, 1023, L, row_base=b)
+        for w2, cols2 in (("sum", {"price": cols["price"]}), ("group", {"price": cols["price"], "quantity": qk})):
+            sq2 = wd.ShardedQuery(wd.Shard(cols2, b, n), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
+            _, e2, a2, k2 = WORKLOADS[w2]
+            if w2 == "sum":
+                res2 = torch.zeros(2, dtype=torch.float64, device="cuda")
+
+                def step2():
+                    sq2.sum_device(e2, a2, res2)
+            else:
+                def step2():
+                    sq2.group_sum_device(e2, a2, None, 0, 4096)
+            mark(f"secondary {w2}")
+            el2, k2_ms, _ = timed(step2)
+            chk2 = None if args.no_check else self_check(w2, sq2, cols2, n, world, wd, torch)
+            b2 = n * READ_BYTES[w2]
+            secondary[w2] = {"query": WORKLOADS[w2][0], "value": round(n_total * args.steps / el2, 1),
+                             "unit": "rows/s", "ms_per_step": round(el2 / args.steps * 1e3, 4),
+                             "scaling": line_common(args, world, n_total, el2, w2)["scaling"],
+                             "kernel": k2, "kernel_ms": round(k2_ms, 4),
+                             "frac": round(b2 / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk2}
+        del qk
+    if rank == 0:
+        if secondary:
+            line["secondary"] = secondary
         line["cpu_baseline"] = cpu_leg(args, workload) if world == 1 else None
         print(json.dumps(line), flush=True)
     if world > 1:
