@@ -10,7 +10,8 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C -d "$OUT/$C" -o run --output-format csv -- \
-    python3 "$R/bench.py" --workload "$W" --rows "$ROWS" --steps 3 --warmup 1 --no-cpu-baseline > "$OUT/$C.log" 2>&1
+    python3 "$R/bench.py" --workload "$W" --rows "$ROWS" --steps 3 --warmup 1 --no-cpu-baseline --no-check \
+    --no-secondary > "$OUT/$C.log" 2>&1
 done
 python3 "$R/tools/pmc_summary.py" $(find "$OUT" -name "*counter_collection.csv") > "$OUT/summary.json"
 cat "$OUT/summary.json"
