@@ -68,6 +68,7 @@ VARIANTS = {
     "deep_g2": {"WARPDB_COMPACT_GROUPS": "2"},
     "ticket": {"WARPDB_COMPACT_SCHED": "ticket"},
     "deep_retire_acqrel": {"WARPDB_EXTRA_DEFINES": "WX_RETIRE_ACQ_REL=1"},
+    "deep_ticket_single": {"WARPDB_EXTRA_DEFINES": "WX_TICKET_PAIR=0"},
     "static": {"WARPDB_COMPACT_SCHED": "static"},
     "deep_g3": {"WARPDB_COMPACT_GROUPS": "3"},
     "deep_dw8": {"WARPDB_COMPACT_DWAVES": "8"},

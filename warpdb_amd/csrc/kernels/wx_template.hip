@@ -872,6 +872,9 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #ifndef WX_DEEP_NT_STORE
 #define WX_DEEP_NT_STORE 1
 #endif
+#ifndef WX_TICKET_PAIR
+#define WX_TICKET_PAIR 1
+#endif
 #if defined(WX_COMPACT_STATIC) && WX_COMPACT_STATIC == 3
 extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx_project_compact_deep(WxCompactArgs wx_a) {
   const wx_u64 wx_E = (wx_u64)wx_a.epoch << WX_EPOCH_SHIFT;
@@ -884,8 +887,14 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
   const bool control = wave == WX_DWAVES;
   const int wx_dt = tid;
   if (tid == 0) {
-    s_tiles[0] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_tiles[1] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (WX_TICKET_PAIR) {  // one dequeue for both first tiles (the counter word serialises every dequeue)
+      const wx_i64 t0 = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_tiles[0] = t0;
+      s_tiles[1] = t0 + 1;
+    } else {
+      s_tiles[0] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_tiles[1] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
   wx_i64 tile = s_tiles[0];
