@@ -93,6 +93,11 @@ Shard upload_shard(const HostTable &h, int device, int64_t b, int64_t e, hipStre
 
 template <typename F>
 void run_per_device(const std::vector<ShardRange> &shards, F &&fn) {
+  if (shards.size() == 1) {  // one device: on this thread (a thread per query costs tens of µs)
+    DevGuard g(shards[0].device);
+    fn(0, shards[0]);
+    return;
+  }
   std::vector<std::exception_ptr> errs(shards.size());
   std::vector<std::thread> th;
   for (size_t i = 0; i < shards.size(); ++i)
@@ -194,14 +199,19 @@ void allreduce_f64(const std::vector<ShardRange> &shards, const std::vector<doub
 // all-reduce of {sum (f64), count (i64)} across the shards' devices.
 std::pair<double, int64_t> sum_over_shards(const std::vector<ShardRange> &shards, std::vector<Shard> &keep,
                                            const std::string &expr_cuda, const std::string &cond_cuda,
-                                           const HostTable *upload_from) {
+                                           const HostTable *upload_from, std::vector<DeviceBuffer> *cached = nullptr) {
   if (shards.empty()) return {0.0, 0};
-  std::vector<DeviceBuffer> outs(shards.size());
+  std::vector<DeviceBuffer> local;
+  std::vector<DeviceBuffer> &outs = cached ? *cached : local;  // {sum, count} per shard (kept by resident shards)
+  if (outs.size() != shards.size()) {
+    outs.clear();
+    outs.resize(shards.size());
+  }
   std::vector<hipStream_t> streams(shards.size(), nullptr);
   run_per_device(shards, [&](size_t i, const ShardRange &r) {
     streams[i] = device_stream(r.device);
     if (upload_from) keep[i] = upload_shard(*upload_from, r.device, r.begin, r.end, streams[i]);
-    outs[i] = DeviceBuffer(r.device, 16);
+    if (!outs[i].ptr) outs[i] = DeviceBuffer(r.device, 16);
     WxTableView v(keep[i].table);
     wx_launch L = sync_launch(r.device, streams[i]);
     L.flags = WX_F_F64_COUNTS;  // {sum, count} as two doubles; asynchronous until after the collective
@@ -261,6 +271,10 @@ struct ResidentShards::Impl {
   std::vector<Shard> shards;
   std::vector<GroupScratch> group;
   std::vector<TopkScratch> topk;
+  std::vector<DeviceBuffer> sum_out;  // {sum, count} per shard, kept across queries
+  // pinned host staging for the first kStage groups of a GROUP BY result (one
+  // stream sync per query instead of one per small pageable copy)
+  char *stage = nullptr;
   std::mutex mu;  // one query at a time per object (shared workspaces and scratch)
 };
 
@@ -323,7 +337,9 @@ ResidentShards::~ResidentShards() {
     impl_->shards[i] = Shard();
     if (i < impl_->group.size()) impl_->group[i] = GroupScratch();
     if (i < impl_->topk.size()) impl_->topk[i] = TopkScratch();
+    if (i < impl_->sum_out.size()) impl_->sum_out[i] = DeviceBuffer();
   }
+  if (impl_->stage) (void)hipHostFree(impl_->stage);
 }
 
 int64_t ResidentShards::num_rows() const { return impl_->n; }
@@ -456,7 +472,7 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
 
 std::pair<double, int64_t> ResidentShards::sum(const std::string &expr_cuda, const std::string &cond_cuda) const {
   std::lock_guard<std::mutex> lk(impl_->mu);
-  return sum_over_shards(impl_->ranges, impl_->shards, expr_cuda, cond_cuda, nullptr);
+  return sum_over_shards(impl_->ranges, impl_->shards, expr_cuda, cond_cuda, nullptr, &impl_->sum_out);
 }
 
 // GROUP BY over the shards: per device wx_group_partials
@@ -513,6 +529,25 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
                             static_cast<int64_t *>(g0.oc.ptr), static_cast<int64_t *>(g0.ng.ptr), nullptr, err,
                             sizeof(err)),
            err);
+  // the out-of-window count, the group count and the first kStage groups, in
+  // one batch of asynchronous copies behind the combine
+  constexpr int64_t kStage = 4096;
+  if (!impl_->stage) {
+    DevGuard dg(dev0);
+    hip_ok(hipHostMalloc(reinterpret_cast<void **>(&impl_->stage), 16 + kStage * 20), "hipHostMalloc");
+  }
+  char *st = impl_->stage;
+  {
+    DevGuard dg(dev0);
+    hip_ok(hipMemcpyAsync(st, static_cast<double *>(g0.win.ptr) + 2 * W, 8, hipMemcpyDeviceToHost, streams[0]),
+           "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(st + 8, g0.ng.ptr, 8, hipMemcpyDeviceToHost, streams[0]), "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(st + 16, g0.ok.ptr, kStage * 4, hipMemcpyDeviceToHost, streams[0]), "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(st + 16 + kStage * 4, g0.os.ptr, kStage * 8, hipMemcpyDeviceToHost, streams[0]),
+           "hipMemcpyAsync");
+    hip_ok(hipMemcpyAsync(st + 16 + kStage * 12, g0.oc.ptr, kStage * 8, hipMemcpyDeviceToHost, streams[0]),
+           "hipMemcpyAsync");
+  }
   for (size_t i = 0; i < ns; ++i) {  // every shard's device errors (and the collective) complete
     DevGuard dg(ranges[i].device);
     hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
@@ -520,10 +555,7 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
     throw_on(wx_check(&L, err, sizeof(err)), err);
   }
   double n_extra_total = 0;
-  {
-    DevGuard dg(dev0);
-    hip_ok(hipMemcpy(&n_extra_total, static_cast<double *>(g0.win.ptr) + 2 * W, 8, hipMemcpyDeviceToHost), "hipMemcpy");
-  }
+  std::memcpy(&n_extra_total, st, 8);
   DeviceBuffer mk, ms, mc;
   if (n_extra_total > 0) {
     std::map<int32_t, std::pair<double, int64_t>> merged;
@@ -572,12 +604,20 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
   }
   DevGuard dg(dev0);
   int64_t ng = 0;
-  hip_ok(hipMemcpy(&ng, g0.ng.ptr, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+  if (n_extra_total > 0) {  // combined again with the out-of-window groups: read the new result
+    hip_ok(hipMemcpy(&ng, g0.ng.ptr, 8, hipMemcpyDeviceToHost), "hipMemcpy");
+  } else {
+    std::memcpy(&ng, st + 8, 8);
+  }
   if (ng > kCap) throw std::runtime_error("group table / output capacity exceeded");
   res.keys.resize(ng);
   res.sums.resize(ng);
   res.counts.resize(ng);
-  if (ng) {
+  if (ng && n_extra_total == 0 && ng <= kStage) {  // the staged copies hold the whole result
+    std::memcpy(res.keys.data(), st + 16, ng * 4);
+    std::memcpy(res.sums.data(), st + 16 + kStage * 4, ng * 8);
+    std::memcpy(res.counts.data(), st + 16 + kStage * 12, ng * 8);
+  } else if (ng) {
     hip_ok(hipMemcpy(res.keys.data(), g0.ok.ptr, ng * 4, hipMemcpyDeviceToHost), "hipMemcpy");
     hip_ok(hipMemcpy(res.sums.data(), g0.os.ptr, ng * 8, hipMemcpyDeviceToHost), "hipMemcpy");
     hip_ok(hipMemcpy(res.counts.data(), g0.oc.ptr, ng * 8, hipMemcpyDeviceToHost), "hipMemcpy");
