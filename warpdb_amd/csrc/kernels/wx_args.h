@@ -170,6 +170,7 @@ struct WxTopkFinArgs {
   wx_i64 *out_idx;
   float *out_vals;
   wx_i64 *count_out;
+  wx_u32 *g_thresh;  // the scan's grid-wide bound slots: zeroed here for the next query
 };
 
 struct WxFillArgs {

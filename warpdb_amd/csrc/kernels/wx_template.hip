@@ -1777,6 +1777,11 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
 #define WX_FIN_BLOCK 1024
 #define WX_FIN_BATCH 8
 extern "C" __global__ __launch_bounds__(WX_FIN_BLOCK) void wx_topk_finalize(WxTopkFinArgs wx_a) {
+  // the scan has finished (stream order): reset its bound slots for the next
+  // query here instead of a host memset per query
+  if (wx_a.g_thresh && threadIdx.x < WX_TOPK_SLOTS)
+    __hip_atomic_store(wx_a.g_thresh + threadIdx.x * WX_TOPK_SLOT_STRIDE, 0u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   __shared__ wx_u32 s_k[WX_FIN_BLOCK / 64][WX_TOPK_K];
   __shared__ wx_i64 s_i[WX_FIN_BLOCK / 64][WX_TOPK_K];
   __shared__ wx_u32 s_bk[WX_TOPK_K];

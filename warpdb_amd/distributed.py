@@ -208,8 +208,8 @@ def merge_topk_device(keys: torch.Tensor, idx: torch.Tensor, vals: torch.Tensor,
     Returns (keys, rows, vals) of k slots and the global count min(k, total),
     all on the device of `keys` (gloo stages through the host)."""
     dev = keys.device
-    if _single(group):
-        return keys[:k], idx[:k].to(torch.int64), vals[:k], torch.clamp(count.reshape(1).to(torch.int64), max=k)
+    if _single(group):  # one shard's list is final (its count is already <= k)
+        return keys[:k], idx[:k], vals[:k], count.reshape(1)
     rec = torch.zeros(2 * k + 1, dtype=torch.int64, device=dev)
     rec[0:1] = count.reshape(1).to(torch.int64)
     rec[1: 1 + 2 * k: 2] = (_f32_bits(keys[:k]) << 32) | _f32_bits(vals[:k])
