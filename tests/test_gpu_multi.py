@@ -257,6 +257,33 @@ def test_warpdb_multi_gpu_group_and_shared_table():
         db.query_multi_gpu_topk("SELECT price FROM test ORDER BY price DESC LIMIT 40")
 
 
+@pytest.mark.parametrize("rows", [3, 1000])
+def test_warpdb_multi_gpu_topk_ties_nan_signed_zero(rows, tmp_path):
+    """query_multi_gpu_topk on a table with heavy ties, NaN and +/-0.0 (and
+    fewer rows than K): the oracle's order -- better key first, ties by the
+    smaller row, NaN last, -0.0 == +0.0 -- in both directions."""
+    from warpdb_amd import pywarpdb as pw
+
+    i = np.arange(rows)
+    price = ((i // 7) % 13).astype(np.float32) - 6.0
+    price[i % 97 == 5] = np.nan
+    price[i % 89 == 3] = -0.0
+    qty = (i % 5).astype(np.float32)
+    path = tmp_path / "ties.csv"
+    with open(path, "w") as f:
+        f.write("price,quantity\n")
+        for p, q in zip(price.tolist(), qty.tolist()):
+            f.write(("nan" if p != p else repr(p)) + "," + repr(q) + "\n")
+    db = pw.WarpDB(str(path))
+    host = {"price": price, "quantity": qty}
+    for desc in (True, False):
+        sql = f"SELECT price * quantity FROM t WHERE quantity > 0 ORDER BY price {'DESC' if desc else 'ASC'} LIMIT 32"
+        k, r, v = db.query_multi_gpu_topk(sql)
+        ok_, oi, ov = ora.topk(ora.HostTable(host), "price", 32, desc, cond="quantity > 0",
+                               select_expr="price * quantity")
+        assert np.array_equal(r, oi) and np.array_equal(bits(k), bits(ok_)) and np.array_equal(bits(v), bits(ov))
+
+
 def test_two_threads_share_one_warpdb():
     """pywarpdb releases the GIL; both threads use the null stream's
     workspace: the per-workspace lock keeps their sorts apart."""
