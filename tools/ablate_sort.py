@@ -71,8 +71,14 @@ VARIANTS = {
     "lbw4_first": {"WARPDB_RS_LBW": "4", D: "WX_RS_LB_FIRST=1"},
     "lbw4_i28": {"WARPDB_RS_LBW": "4", "WARPDB_RS_ITEMS": "28"},
     "items32_g1": {"WARPDB_RS_ITEMS": "32", D: "WX_RS_RANK_G=1"},
+    "hwide": {"WARPDB_RS_HWIDE": "1"},
+    "hnarrow": {"WARPDB_RS_HWIDE": "0"},
+    "hwide_u2": {"WARPDB_RS_HWIDE": "1", D: "WX_RS_HUNROLL=2"},
+    "hwide_u8": {"WARPDB_RS_HWIDE": "1", D: "WX_RS_HUNROLL=8"},
+    "hwide_nopipe": {"WARPDB_RS_HWIDE": "1", D: "WX_RS_HPIPE=0"},
+    "hwide_u2_nopipe": {"WARPDB_RS_HWIDE": "1", D: "WX_RS_HUNROLL=2,WX_RS_HPIPE=0"},
 }
-KNOBS = (D, "WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW")
+KNOBS = (D, "WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW", "WARPDB_RS_HWIDE")
 n = int(float(sys.argv[1])) if len(sys.argv) > 1 else 10**9
 if len(sys.argv) > 2:
     VARIANTS = {k: v for k, v in VARIANTS.items() if k in sys.argv[2].split(",")}

@@ -148,11 +148,16 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
 // Order-preserving float -> u32 map used by the top-K and sort kernels.
 // -0.0 is canonicalised to +0.0 (they compare equal on the CPU); NaN maps to
 // 0, below every number.
+// Integer-only (the float compares cost a canonicalising add and twice the
+// selects): NaN -> 0, -0.0 -> +0.0's image, negatives complemented,
+// non-negatives with the sign bit set.  Denormals are ordinary values (IEEE
+// mode: nothing here is compiled with flush-to-zero).
 __device__ __forceinline__ wx_u32 f2ord(float f) {
-  if (f != f) return 0u;
-  if (f == 0.0f) f = 0.0f;
   const wx_u32 u = __float_as_uint(f);
-  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+  const wx_u32 a = u & 0x7fffffffu;
+  if (a > 0x7f800000u) return 0u;
+  const wx_u32 v = a == 0u ? 0u : u;
+  return v ^ ((wx_u32)((int)v >> 31) | 0x80000000u);
 }
 __device__ __forceinline__ float ord2f(wx_u32 m) {
   if (m == 0u) return __uint_as_float(0x7fc00000u);
@@ -2109,55 +2114,128 @@ __device__ __forceinline__ void wx_rs_count(wx_u32 *h, wx_u32 x, int lane, int c
   }
 }
 
+#ifndef WX_RS_HWIDE
+#define WX_RS_HWIDE 1  // 1.30 -> 0.66 ms per 1e9 keys with the unconditional, pipelined loads (abl_sort_hwide*.txt)
+#endif
+#ifndef WX_RS_HPIPE
+#define WX_RS_HPIPE 1
+#endif
+#if WX_RS_HWIDE
+// One 1024-thread workgroup per CU with 32 copies of every counter (128 KB):
+// lane l adds to copy l % 32, so the 32 lanes of an LDS cycle always hit 32
+// different banks and never one address -- no digit distribution conflicts.
+#define WX_RS_HBLOCK 1024
+#define WX_RS_HC 32
+template <int KIND, bool ASC>
+__device__ __forceinline__ void wx_rs_count_wide(wx_u32 *h, wx_u32 x, int copy) {
+  const wx_u32 k = wx_rs_key_t<KIND, ASC>(x);
+#pragma unroll
+  for (int p = 0; p < 4; ++p) atomicAdd(&h[(p * 256 + ((k >> (8 * p)) & 255u)) * WX_RS_HC + copy], 1u);
+}
+#define WX_RS_COUNT(x) wx_rs_count_wide<KIND, ASC>(h, (x), copy)
+#else
+#define WX_RS_HBLOCK WX_BLOCK
+#define WX_RS_HC WX_RS_HCOPIES
+#define WX_RS_COUNT(x) wx_rs_count<KIND, ASC>(h, (x), lane, copy)
+#endif
+
 // All four digit histograms in one read: contiguous spans of 16-byte loads
 // (WX_RS_HUNROLL per thread) when the array is 16-byte aligned, scalar
 // loads otherwise; per-workgroup LDS counters, one global add per bin.
 template <int KIND, bool ASC>
 __device__ __forceinline__ void wx_radix_hist_impl(const WxRadixHistArgs &a) {
-  __shared__ wx_u32 h[4 * 256 * WX_RS_HCOPIES];  // [digit][bin][copy]
-  for (int i = threadIdx.x; i < 4 * 256 * WX_RS_HCOPIES; i += WX_BLOCK) h[i] = 0u;
+  __shared__ wx_u32 h[4 * 256 * WX_RS_HC];  // [digit][bin][copy]
+  for (int i = threadIdx.x; i < 4 * 256 * WX_RS_HC; i += WX_RS_HBLOCK) h[i] = 0u;
   __syncthreads();
   const int lane = threadIdx.x & 63;
-  const int copy = lane % WX_RS_HCOPIES;
+  const int copy = lane % WX_RS_HC;
+  (void)lane;
   if (a.aligned) {
     typedef wx_u32 u4 __attribute__((ext_vector_type(4)));
     const u4 *q = reinterpret_cast<const u4 *>(a.src);
     const wx_i64 nq = a.n >> 2;
-    const wx_i64 span = (wx_i64)WX_BLOCK * WX_RS_HUNROLL;
-    for (wx_i64 base = (wx_i64)blockIdx.x * span; base < nq; base += (wx_i64)gridDim.x * span) {
+    const wx_i64 span = (wx_i64)WX_RS_HBLOCK * WX_RS_HUNROLL;
+    const wx_i64 stride = (wx_i64)gridDim.x * span;
+    wx_i64 base = (wx_i64)blockIdx.x * span;
+#if WX_RS_HPIPE
+    // Whole spans, software-pipelined as wx_project_dense: the next span's
+    // loads go out before this span is counted (unconditional loads; guarded
+    // ones each wait for the one before and the loop ran latency-bound).
+    if (base + span <= nq) {
+      u4 v[WX_RS_HUNROLL], w[WX_RS_HUNROLL];
+#pragma unroll
+      for (int u = 0; u < WX_RS_HUNROLL; ++u) w[u] = wx::ldv(q + base + (wx_i64)u * WX_RS_HBLOCK + threadIdx.x);
+      __builtin_amdgcn_s_waitcnt(0x0f70);  // the loop head inherits no pending loads
+#pragma unroll
+      for (int u = 0; u < WX_RS_HUNROLL; ++u) v[u] = w[u];
+      while (true) {
+        const wx_i64 nb = base + stride;
+        const bool more = nb + span <= nq;  // workgroup-uniform
+        if (more) {
+#pragma unroll
+          for (int u = 0; u < WX_RS_HUNROLL; ++u) w[u] = wx::ldv(q + nb + (wx_i64)u * WX_RS_HBLOCK + threadIdx.x);
+        }
+#pragma unroll
+        for (int u = 0; u < WX_RS_HUNROLL; ++u) {
+          WX_RS_COUNT(v[u].x);
+          WX_RS_COUNT(v[u].y);
+          WX_RS_COUNT(v[u].z);
+          WX_RS_COUNT(v[u].w);
+        }
+        base = nb;
+        if (!more) break;
+#pragma unroll
+        for (int u = 0; u < WX_RS_HUNROLL; ++u) v[u] = w[u];
+      }
+    }
+#endif
+    for (; base < nq; base += stride) {
       u4 v[WX_RS_HUNROLL];
+      if (base + span <= nq) {  // workgroup-uniform: unconditional loads, all in flight together
+#pragma unroll
+        for (int u = 0; u < WX_RS_HUNROLL; ++u) v[u] = wx::ldv(q + base + (wx_i64)u * WX_RS_HBLOCK + threadIdx.x);
+#pragma unroll
+        for (int u = 0; u < WX_RS_HUNROLL; ++u) {
+          WX_RS_COUNT(v[u].x);
+          WX_RS_COUNT(v[u].y);
+          WX_RS_COUNT(v[u].z);
+          WX_RS_COUNT(v[u].w);
+        }
+        continue;
+      }
 #pragma unroll
       for (int u = 0; u < WX_RS_HUNROLL; ++u) {
-        const wx_i64 i = base + (wx_i64)u * WX_BLOCK + threadIdx.x;
+        const wx_i64 i = base + (wx_i64)u * WX_RS_HBLOCK + threadIdx.x;
         if (i < nq) v[u] = wx::ldv(q + i);
       }
 #pragma unroll
       for (int u = 0; u < WX_RS_HUNROLL; ++u) {
-        if (base + (wx_i64)u * WX_BLOCK + threadIdx.x < nq) {
-          wx_rs_count<KIND, ASC>(h, v[u].x, lane, copy);
-          wx_rs_count<KIND, ASC>(h, v[u].y, lane, copy);
-          wx_rs_count<KIND, ASC>(h, v[u].z, lane, copy);
-          wx_rs_count<KIND, ASC>(h, v[u].w, lane, copy);
+        if (base + (wx_i64)u * WX_RS_HBLOCK + threadIdx.x < nq) {
+          WX_RS_COUNT(v[u].x);
+          WX_RS_COUNT(v[u].y);
+          WX_RS_COUNT(v[u].z);
+          WX_RS_COUNT(v[u].w);
         }
       }
     }
-    if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) wx_rs_count<KIND, ASC>(h, a.src[nq * 4 + threadIdx.x], lane, copy);
+    if (blockIdx.x == 0 && threadIdx.x < (a.n & 3)) WX_RS_COUNT(a.src[nq * 4 + threadIdx.x]);
   } else {
-    for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.n; i += (wx_i64)gridDim.x * WX_BLOCK)
-      wx_rs_count<KIND, ASC>(h, wx::ldv(a.src + i), lane, copy);
+    for (wx_i64 i = (wx_i64)blockIdx.x * WX_RS_HBLOCK + threadIdx.x; i < a.n; i += (wx_i64)gridDim.x * WX_RS_HBLOCK)
+      WX_RS_COUNT(wx::ldv(a.src + i));
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 4 * 256; i += WX_BLOCK) {
+  for (int i = threadIdx.x; i < 4 * 256; i += WX_RS_HBLOCK) {
     wx_u32 c = 0u;
+    // rotated so that the 32 lanes of an LDS cycle read 32 banks
 #pragma unroll
-    for (int j = 0; j < WX_RS_HCOPIES; ++j) c += h[i * WX_RS_HCOPIES + j];
+    for (int j = 0; j < WX_RS_HC; ++j) c += h[i * WX_RS_HC + ((j + i) & (WX_RS_HC - 1))];
     if (c) atomicAdd(&a.hist[i], c);
   }
 }
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_f_a(WxRadixHistArgs a) { wx_radix_hist_impl<0, true>(a); }
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_f_d(WxRadixHistArgs a) { wx_radix_hist_impl<0, false>(a); }
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_i_a(WxRadixHistArgs a) { wx_radix_hist_impl<1, true>(a); }
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_radix_hist_i_d(WxRadixHistArgs a) { wx_radix_hist_impl<1, false>(a); }
+extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_f_a(WxRadixHistArgs a) { wx_radix_hist_impl<0, true>(a); }
+extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_f_d(WxRadixHistArgs a) { wx_radix_hist_impl<0, false>(a); }
+extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_i_a(WxRadixHistArgs a) { wx_radix_hist_impl<1, true>(a); }
+extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_i_d(WxRadixHistArgs a) { wx_radix_hist_impl<1, false>(a); }
 
 #ifndef WX_RS_DIAG_NO_LOOKBACK
 #define WX_RS_DIAG_NO_LOOKBACK 0  // diagnostic: every tile takes its offset as 0 (results invalid)
