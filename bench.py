@@ -35,6 +35,7 @@ import argparse
 import json
 import os
 import platform
+import re
 import subprocess
 import sys
 import time
@@ -395,7 +396,16 @@ def main_ranks(args):
     elif workload == "sort":
         out_v = torch.empty(max(1, n), dtype=torch.float32, device="cuda")
 
+        # ORDER BY a bare float column with no WHERE: the sort reads the column
+        # (the projection would be a copy), as WarpDB::query_sql does
+        bare = re.fullmatch(r"(\w+)\[idx\]", expr)
+        src = cols[bare.group(1)] if bare and bare.group(1) in cols and cols[bare.group(1)].dtype == torch.float32 \
+            else None
+
         def step():
+            if src is not None:
+                wx.sort_float_from(src.data_ptr(), out_v.data_ptr(), n, True, sq.launch)  # synchronous
+                return
             wx.project_filter(sq.table, expr, None, sq.launch_aux, wx.MODE_COMPACT, out_v.data_ptr(), 0, 4, 0,
                               d_count=counts.data_ptr())
             wx.sort_float(out_v.data_ptr(), n, True, sq.launch)  # synchronous, as jit_sort_float
@@ -476,6 +486,10 @@ def main_ranks(args):
                           "parallelism": f"row-sharded x{world}, one process per GPU"}
         if passing is not None:
             line["config"]["passing_rows_per_gpu"] = passing
+        if workload == "sort":
+            line["config"]["sort_input"] = ("the price column itself (ORDER BY a bare column, no WHERE: no projection "
+                                            "copy, as WarpDB::query_sql)" if src is not None
+                                            else "the compacted projection")
         line["check"] = check
         line["roofline"] = roofline(bytes_per_launch, kern_avg_ms, n * rb, kname, pmc_traffic(workload, n),
                                     "HIP events around the dominant kernel on its stream (max over ranks)")

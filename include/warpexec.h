@@ -14,6 +14,7 @@
  *   wx_group_sum        jit_group_sum            include/jit.hpp:15-18, src/jit.cpp:179-246
  *   wx_sort_pairs       jit_sort_pairs           include/jit.hpp:22-23, src/jit.cpp:248-281
  *   wx_sort_float       jit_sort_float           include/jit.hpp:26-27, src/jit.cpp:283-307
+ *   wx_sort_float_from  projection + jit_sort_float of ORDER BY <column>  src/warpdb.cpp:450-455
  *   wx_sort_by_key      ORDER BY <expr> keyed sort  src/warpdb.cpp:470-476
  *   wx_topk             jit_sort_float + LIMIT   src/warpdb.cpp:453-455,483-495
  *   wx_reduce_sum       per-shard SUM of query_multi_gpu (new; the reference
@@ -209,6 +210,14 @@ wx_status wx_sort_pairs(int32_t *d_keys, float *d_vals, int64_t count, int32_t a
                         const wx_launch *launch, char *err, size_t errlen);
 wx_status wx_sort_float(float *d_vals, int64_t count, int32_t ascending, const wx_launch *launch,
                         char *err, size_t errlen);
+/* As wx_sort_float, reading the keys from d_src (not written) and leaving
+ * the sorted keys in d_dst: ORDER BY a bare float column with no WHERE sorts
+ * straight out of the column instead of projecting a copy first
+ * (query_sql's projection + jit_sort_float, src/warpdb.cpp:450-455,
+ * src/jit.cpp:283-307).  d_src == d_dst sorts in place; partial overlap is
+ * refused. */
+wx_status wx_sort_float_from(const float *d_src, float *d_dst, int64_t count, int32_t ascending,
+                             const wx_launch *launch, char *err, size_t errlen);
 /* Stable sort of float keys carrying a 4-byte payload (the ORDER BY key of
  * each selected row and its SELECT value: the keyed sort query_sql intends,
  * src/warpdb.cpp:470-476).  Same order as wx_sort_float: NaN keys last,

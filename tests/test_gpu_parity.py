@@ -548,6 +548,33 @@ def test_sort_float_stable_nan_signed_zero(n, sort, monkeypatch):
         assert np.array_equal(bits(t.cpu().numpy()), bits(ref))
 
 
+@pytest.mark.parametrize("sort,n,data", [("radix", n, "mixed") for n in (1, 2, 8191, 16385, 3 * 16384 + 1, 1_000_003)]
+                         + [("radix", 70_001, "constant"), ("radix", 70_001, "small_ints"),
+                            ("bitonic", 8191, "mixed")])
+def test_sort_float_from_column(sort, n, data, monkeypatch):
+    # ORDER BY a bare column: the sort reads the column and writes a separate
+    # buffer; the result equals the in-place sort's bit for bit, the column is
+    # untouched, whatever number of passes runs (constant keys skip all four,
+    # small integers three) and whichever buffer the last pass lands in
+    monkeypatch.setenv("WARPDB_SORT", sort)
+    if data == "mixed":
+        v = _sort_input(n, 23)
+    elif data == "constant":
+        v = np.full(n, 7.5, dtype=np.float32)
+    else:
+        v = synth.uniform_int(n, 9, 0, 99).astype(np.float32)
+    for asc in (True, False):
+        src = torch.from_numpy(v.copy()).cuda()
+        dst = torch.full((n,), 12345.0, device="cuda")
+        wx.sort_float_from(src.data_ptr(), dst.data_ptr(), n, asc, launch())
+        ref = v[np.argsort(v if asc else -v, kind="stable")]
+        assert np.array_equal(bits(dst.cpu().numpy()), bits(ref))
+        assert np.array_equal(bits(src.cpu().numpy()), bits(v)), "the source column was written"
+        same = torch.from_numpy(v.copy()).cuda()  # src == dst: in place
+        wx.sort_float_from(same.data_ptr(), same.data_ptr(), n, asc, launch())
+        assert np.array_equal(bits(same.cpu().numpy()), bits(ref))
+
+
 @pytest.mark.parametrize("n", [10240, 10241, 12288, 12289, 2 * 10240 + 1, 100_003, 2_500_001])
 @pytest.mark.parametrize("span", ["narrow", "full"])
 def test_sort_pairs_radix_stable(n, span):

@@ -151,6 +151,11 @@ def test_query_sql_order_by_other_expression(tmp_path):
         assert np.array_equal(np.array(got, np.float32), rv)
         got = db.query_sql(f"SELECT quantity * 2 FROM t WHERE price > 15 ORDER BY price {d} OFFSET 7 LIMIT 100")
         assert np.array_equal(np.array(got, np.float32), rv[7:107])
+        # ORDER BY the bare column, no WHERE / LIMIT: the sort reads the column
+        # directly (wx_sort_float_from); the table must be left unchanged
+        _, _, rv = ora.topk(ht, "price", n, desc)
+        assert np.array_equal(np.array(db.query_sql(f"SELECT price FROM t ORDER BY price {d}"), np.float32), rv)
+    assert np.array_equal(np.array(db.query("price"), np.float32), cols["price"])
     # same expression, LIMIT beyond the top-K kernel's 32: full sort + slice
     _, _, rv = ora.topk(ht, "price", 100, True)
     assert np.array_equal(np.array(db.query_sql("SELECT price FROM t ORDER BY price DESC LIMIT 100"), np.float32), rv)

@@ -55,6 +55,7 @@ EXPORTED_SYMBOLS = (
     "wx_topk",
     "wx_sort_pairs",
     "wx_sort_float",
+    "wx_sort_float_from",
     "wx_sort_by_key",
     "wx_sort_float_limit",
     "wx_sort_by_key_limit",
@@ -129,6 +130,7 @@ def load() -> ctypes.CDLL:
         "wx_topk": [T, E, E, E, I32, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_sort_pairs": [P, P, I64, I32, L, E, S],
         "wx_sort_float": [P, I64, I32, L, E, S],
+        "wx_sort_float_from": [P, P, I64, I32, L, E, S],
         "wx_sort_by_key": [P, P, I64, I32, L, E, S],
         "wx_sort_float_limit": [P, I64, I64, I32, L, E, S],
         "wx_sort_by_key_limit": [P, P, I64, I64, I32, L, E, S],
@@ -339,6 +341,14 @@ def sort_by_key(d_keys: int, d_vals: int, count: int, ascending: bool, launch: W
     lib = load()
     err = _err()
     _check(lib.wx_sort_by_key(d_keys, d_vals, count, 1 if ascending else 0, ctypes.byref(launch), err, len(err)), err)
+
+
+def sort_float_from(d_src: int, d_dst: int, count: int, ascending: bool, launch: WxLaunch) -> None:
+    """Sorted copy of d_src's float keys into d_dst (d_src is not written)."""
+    lib = load()
+    err = _err()
+    _check(lib.wx_sort_float_from(d_src, d_dst, count, 1 if ascending else 0, ctypes.byref(launch), err, len(err)),
+           err)
 
 
 def sort_float_limit(d_vals: int, count: int, limit: int, ascending: bool, launch: WxLaunch) -> None:

@@ -609,9 +609,23 @@ std::vector<float> WarpDB::query_sql(const std::string &sql) {
              err);
     return slice(download(dv.ptr, m, table_.device));
   }
-  // projection of the WHERE rows in row order (ordered compaction)
   const int64_t n = table_.num_rows;
   DeviceBuffer dv(table_.device, sizeof(float) * static_cast<size_t>(n ? n : 1));
+  // ORDER BY a bare float column, no WHERE, no LIMIT: the projection would be
+  // a copy of the column, so the sort reads the column itself
+  // (src/warpdb.cpp:450-455 projects, then jit_sort_float sorts the copy)
+  if (ob && !ast.distinct && !ast.limit && cond.empty() && same_expr(ob, sel)) {
+    if (auto var = dynamic_cast<const VariableNode *>(sel)) {
+      for (const auto &c : table_.columns) {
+        if (c.name != var->name || c.type != DataType::Float32) continue;
+        throw_on(wx_sort_float_from(static_cast<const float *>(c.device_ptr), static_cast<float *>(dv.ptr), n,
+                                    ast.order_by->ascending ? 1 : 0, &L, err, sizeof(err)),
+                 err);
+        return slice(download(dv.ptr, n, table_.device));
+      }
+    }
+  }
+  // projection of the WHERE rows in row order (ordered compaction)
   int64_t count = 0;
   throw_on(wx_project_filter(&v.table, sel_c.c_str(), cond.c_str(), &L, WX_MODE_COMPACT, static_cast<float *>(dv.ptr),
                              nullptr, 0, 0, nullptr, &count, err, sizeof(err)),
