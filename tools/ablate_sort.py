@@ -76,6 +76,7 @@ VARIANTS = {
     "hwide_u2": {"WARPDB_RS_HWIDE": "1", D: "WX_RS_HUNROLL=2"},
     "hwide_u8": {"WARPDB_RS_HWIDE": "1", D: "WX_RS_HUNROLL=8"},
     "hwide_nopipe": {"WARPDB_RS_HWIDE": "1", D: "WX_RS_HPIPE=0"},
+    "nt_store": {D: "WX_RS_NT_STORE=1"},
     "hwide_u2_nopipe": {"WARPDB_RS_HWIDE": "1", D: "WX_RS_HUNROLL=2,WX_RS_HPIPE=0"},
 }
 KNOBS = (D, "WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW", "WARPDB_RS_HWIDE")
