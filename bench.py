@@ -65,6 +65,7 @@ WORKLOADS = {
 }
 # bytes every row reads from HBM (the "HBM-read roofline" of BASELINE.md)
 READ_BYTES = {"project": 8, "dense": 8, "group": 8, "sum": 4, "topk": 4, "sort": 4}
+C4_TOTAL_ROWS = 8e9  # BASELINE.json configs[3]: 8B rows row-sharded over 1/2/4/8 GPUs
 
 
 def parse():
@@ -82,6 +83,10 @@ def parse():
     p.add_argument("--no-check", action="store_true", help="skip the post-timing result check")
     p.add_argument("--no-secondary", action="store_true",
                    help="project only: skip the SUM / GROUP BY lines measured beside the headline")
+    p.add_argument("--no-c4", action="store_true",
+                   help="project only: skip the strong-scaled C4 SUM line (8e9 rows over all GPUs)")
+    p.add_argument("--c4-rows", type=float, default=C4_TOTAL_ROWS,
+                   help="rows over all GPUs of the C4 SUM line (BASELINE: 8e9)")
     return p.parse_args()
 
 
@@ -521,6 +526,31 @@ def main_ranks(args):
                              "kernel": k2, "kernel_ms": round(k2_ms, 4),
                              "frac": round(b2 / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk2}
         del qk
+        # C4 exactly as BASELINE states it: 8e9 rows over all ranks (strong
+        # scaling, 8e9 / N per GPU; 32 GB resident at N = 1), SUM + all-reduce,
+        # so the driver's 1/2/4/8-GPU runs measure C4's scaling curve.
+        if not args.no_c4:
+            c4_total = int(args.c4_rows)
+            b4, e4 = wd.shard_range(c4_total, world, rank)
+            n4 = e4 - b4
+            p4 = torch.empty(max(1, n4), dtype=torch.float32, device="cuda")[:n4]
+            wx.fill_synthetic(p4.data_ptr(), wx.FLOAT32, n4, 1, 0, 0.0, 40.0, L, row_base=b4)
+            sq4 = wd.ShardedQuery(wd.Shard({"price": p4}, b4, n4), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
+            _, e4x, a4x, k4 = WORKLOADS["sum"]
+            res4 = torch.zeros(2, dtype=torch.float64, device="cuda")
+
+            def step4():
+                sq4.sum_device(e4x, a4x, res4)
+            mark("secondary c4")
+            el4, k4_ms, _ = timed(step4)
+            chk4 = None if args.no_check else self_check("sum", sq4, {"price": p4}, n4, world, wd, torch)
+            secondary["c4_sum_strong"] = {
+                "query": WORKLOADS["sum"][0], "config": f"C4: {c4_total:.3g} rows over all GPUs (strong scaling)",
+                "total_rows": c4_total, "rows_per_gpu": n4, "value": round(c4_total * args.steps / el4, 1),
+                "unit": "rows/s", "ms_per_step": round(el4 / args.steps * 1e3, 4), "scaling": "strong",
+                "kernel": k4, "kernel_ms": round(k4_ms, 4),
+                "frac": round(n4 * READ_BYTES["sum"] / (k4_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk4}
+            del p4, sq4
     if rank == 0:
         if secondary:
             line["secondary"] = secondary

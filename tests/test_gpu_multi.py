@@ -322,7 +322,7 @@ def test_two_threads_share_one_warpdb():
 
 
 @pytest.mark.parametrize("args", [
-    ["--workload", "project"], ["--workload", "sum", "--total-rows", "3000001"], ["--workload", "group"],
+    ["--workload", "project", "--c4-rows", "3000001"], ["--workload", "sum", "--total-rows", "3000001"], ["--workload", "group"],
     ["--workload", "topk"], ["--workload", "dense"], ["--workload", "sort"],
     ["--workload", "sum", "--api", "--total-rows", "3000001"], ["--workload", "group", "--api"],
     ["--workload", "topk", "--api"]])
@@ -339,3 +339,8 @@ def test_bench_json_contract(args):
     assert line["scaling"] == ("strong" if "--total-rows" in args else "weak")
     if "--api" not in args:  # the bench's own post-timing check of the exchanged result
         assert str(line["check"]).startswith("ok"), line["check"]
+    if args[1] == "project":  # SUM, GROUP BY and C4's strong-scaled SUM measured beside the headline
+        sec = line["secondary"]
+        assert set(sec) == {"sum", "group", "c4_sum_strong"}, sec
+        assert all(str(v["check"]).startswith("ok") and v["value"] > 0 for v in sec.values()), sec
+        assert sec["c4_sum_strong"]["total_rows"] == 3000001 and sec["c4_sum_strong"]["scaling"] == "strong"

@@ -248,7 +248,7 @@ def test_sharded_query_single_rank():
 
 
 @pytest.mark.parametrize("workload,extra", [
-    ("project", ["--rows", "1e7"]),
+    ("project", ["--rows", "1e7", "--c4-rows", "20000001"]),
     ("sum", ["--total-rows", "20000001"]),  # C4's strong-scaling form, ragged shards
     ("group", ["--rows", "5e6"]),           # the dense-window all-reduce
     ("topk", ["--rows", "5e6"]),
@@ -278,6 +278,8 @@ def test_bench_two_ranks_on_one_gpu(workload, extra):
     if workload == "project":
         assert d["config"]["total_rows"] == 2 * 10**7 and d["scaling"] == "weak"
         assert d["config"]["passing_rows_per_gpu"] > 0.6 * 10**7
+        c4 = d["secondary"]["c4_sum_strong"]  # C4's strong-scaled SUM beside the headline
+        assert c4["total_rows"] == 20000001 and c4["rows_per_gpu"] == 10000001 and str(c4["check"]).startswith("ok")
     if workload == "sum":
         assert d["config"]["total_rows"] == 20000001 and d["scaling"] == "strong"
         assert d["config"]["rows_per_gpu"] == 10000001
