@@ -189,6 +189,44 @@ __global__ __launch_bounds__(256) void r2wd(const v4f *__restrict__ a, const v4f
   }
 }
 
+// as r2wd, but the output run goes through buffer stores with an explicit
+// cache policy (aux: 0 plain, 2 nt, 16 sc1, 17 sc0 sc1, 18 sc1 nt); the
+// buffer base is the workgroup's output run, lanes store at 16-B offsets
+template <int U, int AUX, bool READ>
+__global__ __launch_bounds__(256) void r2wdb(const v4f *__restrict__ a, const v4f *__restrict__ b,
+                                             v4f *__restrict__ ov, v4u *__restrict__ oi, size_t nq) {
+  const size_t span = (size_t)256 * U;
+  const size_t ospan = span * 5 / 8;
+  for (size_t base = (size_t)blockIdx.x * span, ob = (size_t)blockIdx.x * ospan; base + span <= nq;
+       base += (size_t)gridDim.x * span, ob += (size_t)gridDim.x * ospan) {
+    v4f acc = {1.f, 2.f, 3.f, (float)base};
+    if (READ) {
+      v4f va[U], vb[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const size_t i = base + u * 256 + threadIdx.x;
+        va[u] = __builtin_nontemporal_load(a + i);
+        vb[u] = __builtin_nontemporal_load(b + i);
+      }
+      acc = va[0] * vb[0];
+#pragma unroll
+      for (int u = 1; u < U; ++u) acc += va[u] * vb[u];
+    }
+    __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(ov + ob, 0, 0x7fffffff, 0x00020000);
+    __amdgpu_buffer_rsrc_t ri = __builtin_amdgcn_make_buffer_rsrc(oi + ob, 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const unsigned k = u * 256 + threadIdx.x;
+      if (k < ospan) {
+        const v4u x = __builtin_bit_cast(v4u, acc);
+        const v4u y = (v4u){k, k + 1, k + 2, k + 3};
+        __builtin_amdgcn_raw_buffer_store_b128(x, rv, (int)(k * 16), 0, AUX);
+        __builtin_amdgcn_raw_buffer_store_b128(y, ri, (int)(k * 16), 0, AUX);
+      }
+    }
+  }
+}
+
 // as r2wd, but the output run is written with 4-byte stores (one value per
 // lane, like the compaction's LDS drain), starting `shift` floats past a
 // 16-byte boundary
@@ -316,6 +354,19 @@ int main(int argc, char **argv) {
   }
   RUN("read1c u8 nt", (read1c<8, true>), n * 4, (const v4f *)a, nq, out);
   RUN("r2wd u8", (r2wd<8>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+  if (getenv("BW_POLICY")) {
+    RUN("r2wdb plain", (r2wdb<8, 0, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    RUN("r2wdb nt", (r2wdb<8, 2, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    RUN("r2wdb sc1", (r2wdb<8, 16, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    RUN("r2wdb sc0sc1", (r2wdb<8, 17, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    RUN("r2wdb sc1nt", (r2wdb<8, 18, true>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    RUN("w-only plain", (r2wdb<8, 0, false>), n * 5, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    RUN("w-only nt", (r2wdb<8, 2, false>), n * 5, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    RUN("w-only sc1", (r2wdb<8, 16, false>), n * 5, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    RUN("w-only sc0sc1", (r2wdb<8, 17, false>), n * 5, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    RUN("r2wd u8 (again)", (r2wd<8>), n * 13, (const v4f *)a, (const v4f *)b, (v4f *)ov, (v4u *)oi, nq);
+    return 0;
+  }
   {
     int wp1[] = {1};
     for (int w : wp1) {
