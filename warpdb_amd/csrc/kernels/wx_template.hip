@@ -976,6 +976,9 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
       const wx_i64 prev_base = wx_a.row_base + tile2 * WX_TILE;
       const float *sv = s_val[cur];
       const unsigned short *so = s_off[cur];
+#if WX_DIAG_NO_STORE  // diagnostic: timing only (results invalid), the LDS stage still read
+      if (excl == -1 && wx_a.out_val) wx_a.out_val[0] = sv[wx_dt] + (float)so[wx_dt];
+#else
       const wx_i64 end = excl + (wx_i64)tot2;
       wx_i64 b0 = (excl + 31) & ~(wx_i64)31;
       if (b0 > end) b0 = end;
@@ -1016,6 +1019,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
           }
         }
       }
+#endif
     }
     __syncthreads();
     // phase 3: data waves stage t_k into buffer cur; the control wave
@@ -1023,10 +1027,14 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     if (control) {
       if (have1) {
         wx_i64 excl = 0;
+#if WX_DIAG_NO_LOOKBACK  // diagnostic: timing only (results invalid)
+        excl = WX_DIAG_NO_LOOKBACK == 2 ? tile1 * WX_TILE * 5 / 8 + 3 : tile1 * WX_TILE / 2;
+#else
         if (tile1 > 0) {
           excl = wx_lookback(wx_a, tile1);
           if (lane == 0) wx::st_agent(&wx_a.status[tile1], wx_E | WX_FLAG_P | (wx_u64)(excl + tot1));
         }
+#endif
         if (lane == 0) {
           s_excl[cur ^ 1] = excl;  // read when t_{k-1} is written, in iteration k + 1
           if (tile1 == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + tot1;
