@@ -629,6 +629,27 @@ def test_sort_float_unaligned_view(n):
     assert buf[0].item() == -123.0
 
 
+@pytest.mark.parametrize("n", [5, 16385, 400_007])
+@pytest.mark.parametrize("src_off,dst_off", [(1, 0), (0, 3), (2, 1)])
+def test_sort_float_from_unaligned(n, src_off, dst_off):
+    # ORDER BY a bare column whose source and destination start 4-12 bytes
+    # past a 16-byte boundary (independently): the column-reading histogram
+    # and first pass take their scalar paths; neighbours stay untouched
+    v = _sort_input(n, 37)
+    sbuf = torch.full((n + 4,), -321.0, dtype=torch.float32, device="cuda")
+    sbuf[src_off:src_off + n].copy_(torch.from_numpy(v))
+    dbuf = torch.full((n + 4,), -654.0, dtype=torch.float32, device="cuda")
+    for asc in (True, False):
+        wx.sort_float_from(sbuf[src_off:].data_ptr(), dbuf[dst_off:].data_ptr(), n, asc, launch())
+        ref = v[np.argsort(v if asc else -v, kind="stable")]
+        assert np.array_equal(bits(dbuf[dst_off:dst_off + n].cpu().numpy()), bits(ref))
+        assert np.array_equal(bits(sbuf[src_off:src_off + n].cpu().numpy()), bits(v)), "the column was written"
+        d = dbuf.cpu().numpy()
+        assert np.all(d[:dst_off] == -654.0) and np.all(d[dst_off + n:] == -654.0)
+        s = sbuf.cpu().numpy()
+        assert np.all(s[:src_off] == -321.0) and np.all(s[src_off + n:] == -321.0)
+
+
 @pytest.mark.parametrize("sort,n", [("radix", n) for n in (1, 12289, 1_000_003)]
                          + [("bitonic", n) for n in (1, 12289)])
 def test_sort_by_key_stable(n, sort, monkeypatch):
