@@ -35,7 +35,9 @@ VARIANTS = {
     "rank_g4": {D: "WX_RS_RANK_G=4"},
     "rank_lead0": {D: "WX_RS_RANK_LEAD=0"},
     "lb_first": {D: "WX_RS_LB_FIRST=1"},
+    "lbw1": {"WARPDB_RS_LBW": "1"},
     "lbw2": {"WARPDB_RS_LBW": "2"},
+    "lbw3": {"WARPDB_RS_LBW": "3"},
     "lbw2_first": {"WARPDB_RS_LBW": "2", D: "WX_RS_LB_FIRST=1"},
     "hcopies4": {D: "WX_RS_HCOPIES=4"},
     "hcopies16": {D: "WX_RS_HCOPIES=16"},
