@@ -253,7 +253,9 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 // (profiles/r01/ablate_dense.txt).  The software-pipelined loop below (4
 // quads per thread, 3 workgroups per CU) takes 2.12 ms against 2.165 for the
 // best unpipelined geometry (profiles/r02/abl_dense_*.txt).  Without fill
-// every partially selected 64-B line is a masked write: 3.1 ms.
+// every partially selected 64-B line was a masked write (3.1 ms); masked mode
+// now reads and rewrites whole quads instead (WX_DENSE_BLEND: 2.86 ms,
+// profiles/r02/abl_dense_masked_1e9.txt).
 #ifndef WX_UNROLL
 #define WX_UNROLL 4
 #endif
@@ -263,8 +265,20 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 #ifndef WX_DENSE_PIPE
 #define WX_DENSE_PIPE 1
 #endif
-// One span's rows: evaluate and store (full spans: one 16-byte store per quad).
-#define WX_DENSE_SPAN_OUT(FULL)                                                                        \
+#ifndef WX_DENSE_BLEND
+// Masked mode (rows failing the WHERE keep their old value, the reference's
+// jit_compile_and_launch contract): whole spans read the output quads with
+// the columns and write every quad back whole, old values where the row
+// fails.  16 B/row of traffic instead of 12, but no partial-line (masked)
+// writes, which cost more than the extra read.
+#define WX_DENSE_BLEND 1
+#endif
+#ifndef WX_DENSE_BLEND_NT
+#define WX_DENSE_BLEND_NT 1  // nontemporal loads of the old output quads (2.88 vs 2.97 ms, plain)
+#endif
+// One span's rows: evaluate and store (full spans: one 16-byte store per quad;
+// BLEND: full spans of masked mode, wx_old holds the output quads as read).
+#define WX_DENSE_SPAN_OUT(FULL, BLEND)                                                                 \
   _Pragma("unroll") for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {                                   \
     const wx_i64 wx_r0 = WX_QUAD(wx_u) << 2;                                                           \
     if (WX_QUAD(wx_u) >= wx_nq) continue;                                                              \
@@ -278,7 +292,14 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
       wx_o[wx_e] = static_cast<float>(WX_EXPR);                                                        \
     }                                                                                                  \
     const bool wx_all = wx_k[0] && wx_k[1] && wx_k[2] && wx_k[3];                                      \
-    if ((FULL) && (wx_a.fill || wx_all)) {                                                             \
+    if ((FULL) && (BLEND)) {                                                                           \
+      f4 v;                                                                                            \
+      v.x = wx_k[0] ? wx_o[0] : wx_old[wx_u].x;                                                        \
+      v.y = wx_k[1] ? wx_o[1] : wx_old[wx_u].y;                                                        \
+      v.z = wx_k[2] ? wx_o[2] : wx_old[wx_u].z;                                                        \
+      v.w = wx_k[3] ? wx_o[3] : wx_old[wx_u].w;                                                        \
+      ::wx::st_sel<WX_DENSE_NT_STORE>(reinterpret_cast<f4 *>(wx_a.out + wx_r0), v);                   \
+    } else if ((FULL) && (wx_a.fill || wx_all)) {                                                      \
       f4 v;                                                                                            \
       v.x = wx_k[0] ? wx_o[0] : 0.0f;                                                                  \
       v.y = wx_k[1] ? wx_o[1] : 0.0f;                                                                  \
@@ -353,14 +374,19 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
       WX_COLS(WX_MOVE_N)
     }
   }
+  const bool wx_blend = WX_DENSE_BLEND && !wx_every;  // masked mode
   for (; wx_base < wx_nq; wx_base += wx_stride) {
     WX_COLS(WX_DECL_U)
+    f4 wx_old[WX_UNROLL];
     const bool wx_full = WX_ALIGNED16 && wx_base + WX_SPAN <= wx_nfull;
     if (wx_full) {
 #pragma unroll
       for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
         const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;
         WX_COLS(WX_LOAD_U_FAST)
+        if (wx_blend)
+          wx_old[wx_u] = WX_DENSE_BLEND_NT ? __builtin_nontemporal_load(reinterpret_cast<const f4 *>(wx_a.out + wx_r0u))
+                                           : *reinterpret_cast<const f4 *>(wx_a.out + wx_r0u);
       }
     } else {
 #pragma unroll
@@ -369,7 +395,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
         WX_COLS(WX_LOAD_U)
       }
     }
-    WX_DENSE_SPAN_OUT(wx_full)
+    WX_DENSE_SPAN_OUT(wx_full, wx_blend)
   }
 }
 #else
