@@ -31,7 +31,7 @@ table = wx.Table(n, [wx.Column("price", wx.FLOAT32, price.data_ptr()), wx.Column
 out = torch.empty(n, dtype=torch.float32, device="cuda")
 E, C = "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)"
 VARIANTS = {"masked_writes": ("WX_DENSE_BLEND=0", wx.MODE_DENSE), "blend": ("", wx.MODE_DENSE),
-            "blend_plain_old": ("WX_DENSE_BLEND_NT=0", wx.MODE_DENSE),
+            "blend_unpipelined": ("WX_DENSE_BLEND_PIPE=0", wx.MODE_DENSE),
             "fill": ("", wx.MODE_DENSE_FILL)}
 res = {k: [] for k in VARIANTS}
 def setenv(v):

@@ -67,6 +67,10 @@ __device__ __forceinline__ void stv(V *p, V v) {
   *p = v;
 #endif
 }
+template <bool B>
+struct btag {
+  static constexpr bool value = B;
+};
 template <bool NT, typename V>
 __device__ __forceinline__ void st_sel(V *p, V v) {
   if constexpr (NT)
@@ -254,8 +258,8 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 // quads per thread, 3 workgroups per CU) takes 2.12 ms against 2.165 for the
 // best unpipelined geometry (profiles/r02/abl_dense_*.txt).  Without fill
 // every partially selected 64-B line was a masked write (3.1 ms); masked mode
-// now reads and rewrites whole quads instead (WX_DENSE_BLEND: 2.86 ms,
-// profiles/r02/abl_dense_masked_1e9.txt).
+// now reads and rewrites whole quads instead, pipelined like fill mode
+// (WX_DENSE_BLEND: 2.63 vs 3.00 ms, profiles/r02/abl_dense_masked_1e9.txt).
 #ifndef WX_UNROLL
 #define WX_UNROLL 4
 #endif
@@ -272,6 +276,9 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 // fails.  16 B/row of traffic instead of 12, but no partial-line (masked)
 // writes, which cost more than the extra read.
 #define WX_DENSE_BLEND 1
+#endif
+#ifndef WX_DENSE_BLEND_PIPE
+#define WX_DENSE_BLEND_PIPE 1  // masked mode through the software-pipelined loop too
 #endif
 #ifndef WX_DENSE_BLEND_NT
 #define WX_DENSE_BLEND_NT 1  // nontemporal loads of the old output quads (2.88 vs 2.97 ms, plain)
@@ -314,12 +321,13 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
   }
 #if WX_DENSE_PIPE
 // Software-pipelined steady state: while this span and the next are whole
-// and every row is written (fill, or no WHERE), the next span's loads are
+// and every row is written (fill, no WHERE, or masked mode's whole-quad
+// blend), the next span's loads are
 // issued before this span's stores and waited for after them.  On gfx9
 // stores count in vmcnt, so the straight-line body lets the wait leave this
 // span's stores in flight (a conditional store or load anywhere in the loop
-// makes the compiler drain vmcnt to 0).  Ragged spans and masked output take
-// the generic loop below.
+// makes the compiler drain vmcnt to 0).  Ragged spans take the generic loop
+// below.
 #define WX_DECL_N(name, T, slot) T wx_n##slot[WX_UNROLL][4];
 #define WX_LOAD_N_FAST(name, T, slot) ::wx::load4_full<T>(wx_a.col[slot], wx_r0u, wx_n##slot[wx_u]);
 #define WX_MOVE_N(name, T, slot)                                  \
@@ -332,19 +340,29 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
   const wx_i64 wx_stride = (wx_i64)gridDim.x * WX_SPAN;
   wx_i64 wx_base = (wx_i64)blockIdx.x * WX_SPAN;
   const bool wx_every = wx_a.fill || !WX_HAS_COND;
-  if (WX_ALIGNED16 && wx_every && wx_base + WX_SPAN <= wx_nfull) {
+  const bool wx_blend = WX_DENSE_BLEND && !wx_every;  // masked mode
+  // BLEND: masked mode, the output quads load with the columns and failing
+  // rows keep their old value (see WX_DENSE_BLEND)
+  auto wx_pipe = [&](auto wx_tag) {
+    constexpr bool BLEND = decltype(wx_tag)::value;
     WX_COLS(WX_DECL_U)
     WX_COLS(WX_DECL_N)
+    f4 wx_old[WX_UNROLL], wx_nold[WX_UNROLL];
 #pragma unroll
     for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
       const wx_i64 wx_r0u = WX_QUAD(wx_u) << 2;
       WX_COLS(WX_LOAD_N_FAST)
+      if constexpr (BLEND) wx_nold[wx_u] = ::wx::ldv(reinterpret_cast<const f4 *>(wx_a.out + wx_r0u));
     }
     // Drain here, so the loop head inherits no pending loads: otherwise the
     // wait the compiler places there for this prologue (vmcnt(0)) also
     // drains every later iteration's stores.
     __builtin_amdgcn_s_waitcnt(0x0f70);  // gfx9: vmcnt(0) expcnt(7) lgkmcnt(15)
     WX_COLS(WX_MOVE_N)
+    if constexpr (BLEND) {
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) wx_old[wx_u] = wx_nold[wx_u];
+    }
     while (true) {
       const wx_i64 wx_nb = wx_base + wx_stride;
       const bool wx_more = wx_nb + WX_SPAN <= wx_nfull;  // workgroup-uniform
@@ -353,6 +371,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
         for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
           const wx_i64 wx_r0u = (wx_nb + (wx_i64)wx_u * WX_BLOCK + threadIdx.x) << 2;
           WX_COLS(WX_LOAD_N_FAST)
+          if constexpr (BLEND) wx_nold[wx_u] = ::wx::ldv(reinterpret_cast<const f4 *>(wx_a.out + wx_r0u));
         }
       }
 #pragma unroll
@@ -365,16 +384,25 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_project_dense(WxDenseA
           const wx_i64 idx = wx_r0 + wx_e;
           (void)idx;
           const bool wx_k = WX_EVAL_COND();
-          v[wx_e] = wx_k ? static_cast<float>(WX_EXPR) : 0.0f;
+          v[wx_e] = wx_k ? static_cast<float>(WX_EXPR) : (BLEND ? wx_old[wx_u][wx_e] : 0.0f);
         }
         ::wx::st_sel<WX_DENSE_NT_STORE>(reinterpret_cast<f4 *>(wx_a.out + wx_r0), v);
       }
       wx_base = wx_nb;
       if (!wx_more) break;
       WX_COLS(WX_MOVE_N)
+      if constexpr (BLEND) {
+#pragma unroll
+        for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) wx_old[wx_u] = wx_nold[wx_u];
+      }
     }
+  };
+  if (WX_ALIGNED16 && wx_base + WX_SPAN <= wx_nfull) {
+    if (wx_every)
+      wx_pipe(::wx::btag<false>{});
+    else if (WX_DENSE_BLEND_PIPE && wx_blend)
+      wx_pipe(::wx::btag<true>{});
   }
-  const bool wx_blend = WX_DENSE_BLEND && !wx_every;  // masked mode
   for (; wx_base < wx_nq; wx_base += wx_stride) {
     WX_COLS(WX_DECL_U)
     f4 wx_old[WX_UNROLL];
