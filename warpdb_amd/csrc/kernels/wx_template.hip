@@ -322,8 +322,8 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 #if WX_DENSE_PIPE
 // Software-pipelined steady state: while this span and the next are whole
 // and every row is written (fill, no WHERE, or masked mode's whole-quad
-// blend), the next span's loads are
-// issued before this span's stores and waited for after them.  On gfx9
+// blend), the next span's loads are issued before this span's stores and
+// waited for after them.  On gfx9
 // stores count in vmcnt, so the straight-line body lets the wait leave this
 // span's stores in flight (a conditional store or load anywhere in the loop
 // makes the compiler drain vmcnt to 0).  Ragged spans take the generic loop
