@@ -126,6 +126,24 @@ def test_dense_vs_oracle(n, offset):
             assert buf[0].item() == -7.0
 
 
+@pytest.mark.parametrize("mode", ["masked", "fill"])
+def test_dense_many_spans_per_workgroup(mode):
+    # 2^23 + 5 rows: every workgroup walks several whole spans through the
+    # software-pipelined loop (masked mode: old output quads read and blended)
+    # and then the ragged tail; unselected rows keep a per-row sentinel
+    n = (1 << 23) + 5
+    cols = synth.c2_table(n)
+    table, t = dev_table(cols)
+    price, qty = t["price"], t["quantity"]
+    sentinel = torch.arange(n, dtype=torch.float32, device="cuda") * -1.0 - 0.5
+    out = sentinel.clone()
+    m = wx.MODE_DENSE if mode == "masked" else wx.MODE_DENSE_FILL
+    wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", launch(), m, out.data_ptr())
+    keep = sentinel if mode == "masked" else torch.zeros_like(sentinel)
+    want = torch.where(price > 15.0, price * qty, keep)
+    assert torch.equal(out.view(torch.int32), want.view(torch.int32))
+
+
 def test_jit_arch_identity_raw_expression():
     # tests/jit_arch_test.cpp:6-38: the un-lowered expression "price" -> 2.0
     table, _ = dev_table({"price": np.array([2.0], np.float32), "quantity": np.array([0], np.int32)})
