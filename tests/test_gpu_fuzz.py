@@ -124,3 +124,27 @@ def test_random_group_by_vs_oracle(fuzz_table, case):
     assert np.array_equal(cnts[:g].cpu().numpy(), rc), (val, key, cond)
     got = sums[:g].cpu().numpy()
     assert np.all((got == rs) | (np.abs(got - rs) <= 1e-12 * np.maximum(np.abs(rs), 1e-300))), (val, key, cond)
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_random_topk_vs_oracle(fuzz_table, case):
+    # ORDER BY <expr> [DESC] LIMIT k with a random WHERE and SELECT expression
+    # (src/warpdb.cpp:453-495 semantics: the stable order, ties by row): keys,
+    # row ids and selected values bit for bit against the oracle
+    cols, table, _ = fuzz_table
+    rng = np.random.default_rng(300 + case)
+    order = gen_expr(rng, 2)
+    cond = gen_cond(rng) if case % 2 else None
+    sel = gen_expr(rng, 2)
+    k = int(rng.choice([1, 2, 5, 17, 32]))
+    desc = bool(case % 3)
+    keys = torch.empty(k, dtype=torch.float32, device="cuda")
+    idx = torch.empty(k, dtype=torch.int64, device="cuda")
+    vals = torch.empty(k, dtype=torch.float32, device="cuda")
+    m = wx.topk(table, ora.lower(order), ora.lower(cond) if cond else None, ora.lower(sel), k, desc, launch(),
+                keys.data_ptr(), idx.data_ptr(), vals.data_ptr())
+    rk, ri, rv = ora.topk(ora.HostTable(cols), order, k, desc, cond, sel)
+    assert m == len(ri), (order, cond, sel, k, desc)
+    assert np.array_equal(idx[:m].cpu().numpy(), ri), (order, cond, sel, k, desc)
+    assert np.array_equal(bits(keys[:m].cpu().numpy()), bits(rk)), (order, cond, sel, k, desc)
+    assert np.array_equal(bits(vals[:m].cpu().numpy()), bits(rv)), (order, cond, sel, k, desc)
