@@ -344,3 +344,55 @@ def test_bench_json_contract(args):
         assert set(sec) == {"sum", "group", "c4_sum_strong"}, sec
         assert all(str(v["check"]).startswith("ok") and v["value"] > 0 for v in sec.values()), sec
         assert sec["c4_sum_strong"]["total_rows"] == 3000001 and sec["c4_sum_strong"]["scaling"] == "strong"
+
+
+@pytest.mark.parametrize("nshards", [2, 3])
+def test_virtual_shards_on_one_device(nshards, monkeypatch, tmp_path):
+    """The multi-shard C++ path on a one-GPU box: WARPDB_VIRTUAL_SHARDS plans
+    several shards on the visible device(s) (a host thread per shard, the
+    shard plan, per-shard scratch, the merges); co-located shards exchange
+    through the host instead of RCCL.  Every result against the oracle."""
+    from warpdb_amd import pywarpdb as pw
+
+    monkeypatch.setenv("WARPDB_VIRTUAL_SHARDS", str(nshards))
+    n = 1_000_003
+    cols = [("price", pw.DataType.Float32, 1, 0, 0.0, 40.0), ("quantity", pw.DataType.Int32, 3, 1, 0, 1023)]
+    rs_ = pw.ResidentShards.synthetic(n, cols, nshards)
+    assert rs_.num_shards == nshards and rs_.num_rows == n
+    host = synth.c3_table(n)
+    ht = ora.HostTable(host)
+    s, c = rs_.sum("(price[idx] * 0.9f)", "(price[idx] > 20.0f)")
+    es, ec = ora.reduce_sum(ht, "price * 0.9", "price > 20")
+    assert c == ec and abs(s - es) <= 1e-12 * abs(es)
+    for key_lo in (0, 700):  # 700: keys below the window merge as out-of-window groups
+        k, sm, cn = rs_.group_sum("price[idx]", "quantity[idx]", "", key_lo)
+        rk, rsum, rcnt = ora.group_sum(ht, "price", "quantity")
+        assert np.array_equal(k, rk) and np.array_equal(cn, rcnt)
+        np.testing.assert_allclose(sm, rsum, rtol=1e-12, atol=0)
+    for k, desc in ((5, True), (32, False), (1, True)):
+        tk, ti, tv = rs_.topk("price[idx]", "(quantity[idx] < 700)", "(price[idx] * 0.9f)", k, desc)
+        ok_, oi, ov = ora.topk(ht, "price", k, desc, cond="quantity < 700", select_expr="price * 0.9")
+        assert np.array_equal(ti, oi) and np.array_equal(bits(tk), bits(ok_)) and np.array_equal(bits(tv), bits(ov))
+    d = np.asarray(rs_.dense("(price[idx] * 2.0f)", "(price[idx] > 15.0f)"))
+    want = ora.dense(ht, "price * 2", "price > 15", np.zeros(n, np.float32))
+    assert np.array_equal(bits(d), bits(want))
+    # the facade (WarpDB::query_multi_gpu*) over a CSV: shards built from the host table
+    m = 10_007
+    small = synth.c2_table(m)
+    path = tmp_path / "t.csv"
+    with open(path, "w") as f:
+        f.write("price,quantity\n")
+        for p_, q_ in zip(small["price"].tolist(), small["quantity"].tolist()):
+            f.write(f"{p_!r},{q_!r}\n")
+    db = pw.WarpDB(str(path))
+    hs = ora.HostTable({"price": small["price"], "quantity": small["quantity"]})
+    r = np.asarray(db.query_multi_gpu("price * quantity WHERE price > 15"), np.float32)
+    assert np.array_equal(bits(r), bits(ora.dense(hs, "price * quantity", "price > 15", np.zeros(m, np.float32))))
+    s2, c2 = db.query_multi_gpu_sum("price * 0.9 WHERE price > 20")
+    es2, ec2 = ora.reduce_sum(hs, "price * 0.9", "price > 20")
+    assert c2 == ec2 and abs(s2 - es2) <= 1e-12 * abs(es2)
+    k2, rows2, v2 = db.query_multi_gpu_topk("SELECT price FROM t ORDER BY price DESC LIMIT 7")
+    ok2, oi2, ov2 = ora.topk(hs, "price", 7, True, select_expr="price")
+    assert np.array_equal(rows2, oi2) and np.array_equal(bits(v2), bits(ov2))
+    r3 = np.asarray(pw.WarpDB.query_multi_gpu_csv(str(path), "price * quantity WHERE price > 15", 1000), np.float32)
+    assert np.array_equal(bits(r3), bits(r))

@@ -30,18 +30,6 @@
 
 namespace warpdb {
 
-std::vector<ShardRange> plan_shards(int64_t n_rows, int devices) {
-  std::vector<ShardRange> out;
-  if (devices < 1) devices = 1;
-  const int64_t chunk = (n_rows + devices - 1) / devices;
-  for (int d = 0; d < devices; ++d) {
-    const int64_t b = d * chunk, e = std::min(n_rows, b + chunk);
-    if (b >= e) break;
-    out.push_back({d, b, e});
-  }
-  return out;
-}
-
 namespace {
 
 int device_count() {
@@ -51,9 +39,51 @@ int device_count() {
   return n;
 }
 
-// `want` devices (0 = every visible one), checked against what is there
+// Test hook: WARPDB_VIRTUAL_SHARDS=k plans k shards over the visible devices
+// round robin, so with k above the device count several shards share a
+// device and the multi-shard code (a thread per shard, the shard plan,
+// per-shard scratch, the exchanges, the merges) runs on a one-GPU box.
+// Shards that share a device cannot form an RCCL communicator; their
+// exchanges stage through the host (see allreduce_f64, ResidentShards::topk).
+int virtual_shards() {
+  const char *v = std::getenv("WARPDB_VIRTUAL_SHARDS");
+  return v ? std::max(0, std::atoi(v)) : 0;
+}
+
+// shards to plan when the caller asks for every device
+int shard_count() {
+  const int v = virtual_shards();
+  return v > 0 ? v : device_count();
+}
+
+// one shard per device (the RCCL case)
+bool distinct_devices(const std::vector<ShardRange> &shards) {
+  std::vector<int> d;
+  for (const auto &r : shards) d.push_back(r.device);
+  std::sort(d.begin(), d.end());
+  return std::adjacent_find(d.begin(), d.end()) == d.end();
+}
+
+}  // namespace
+
+std::vector<ShardRange> plan_shards(int64_t n_rows, int devices) {
+  std::vector<ShardRange> out;
+  if (devices < 1) devices = 1;
+  const int physical = virtual_shards() > 0 ? device_count() : devices;
+  const int64_t chunk = (n_rows + devices - 1) / devices;
+  for (int d = 0; d < devices; ++d) {
+    const int64_t b = d * chunk, e = std::min(n_rows, b + chunk);
+    if (b >= e) break;
+    out.push_back({d % physical, b, e});
+  }
+  return out;
+}
+
+namespace {
+
+// `want` shards (0 = every visible device), checked against what is there
 int devices_for(int want) {
-  const int have = device_count();
+  const int have = shard_count();
   if (want <= 0) return have;
   if (want > have) throw std::runtime_error("requested " + std::to_string(want) + " devices, " +
                                             std::to_string(have) + " visible");
@@ -181,6 +211,20 @@ void allreduce_f64(const std::vector<ShardRange> &shards, const std::vector<doub
                    const std::vector<hipStream_t> &streams, size_t count) {
   const int nshard = static_cast<int>(shards.size());
   if (nshard < 2) return;
+  if (!distinct_devices(shards)) {  // co-located shards (WARPDB_VIRTUAL_SHARDS): sum through the host
+    std::vector<double> acc(count, 0.0), part(count);
+    for (int i = 0; i < nshard; ++i) {
+      DevGuard g(shards[i].device);
+      hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
+      hip_ok(hipMemcpy(part.data(), bufs[i], count * sizeof(double), hipMemcpyDeviceToHost), "hipMemcpy");
+      for (size_t j = 0; j < count; ++j) acc[j] += part[j];
+    }
+    for (int i = 0; i < nshard; ++i) {
+      DevGuard g(shards[i].device);
+      hip_ok(hipMemcpy(bufs[i], acc.data(), count * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+    }
+    return;
+  }
   Comms &c = comms_for(nshard);
   std::lock_guard<std::mutex> lk(c.mu);
   if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
@@ -240,7 +284,7 @@ std::pair<double, int64_t> sum_over_shards(const std::vector<ShardRange> &shards
 
 std::pair<double, int64_t> run_multi_gpu_sum(const HostTable &host, const std::string &expr_cuda,
                                              const std::string &cond_cuda) {
-  auto shards = plan_shards(host.num_rows(), device_count());
+  auto shards = plan_shards(host.num_rows(), shard_count());
   std::vector<Shard> keep(shards.size());
   auto r = sum_over_shards(shards, keep, expr_cuda, cond_cuda, &host);
   for (size_t i = 0; i < keep.size(); ++i) {
@@ -409,7 +453,19 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
                      reinterpret_cast<int64_t *>(c + kTopkMax * 16), nullptr, err, sizeof(err)),
              err);
   });
-  if (ns > 1) {
+  if (ns > 1 && !distinct_devices(ranges)) {  // co-located shards (WARPDB_VIRTUAL_SHARDS): gather through the host
+    std::vector<char> all(kTopkRec * ns);
+    for (size_t i = 0; i < ns; ++i) {
+      DevGuard g(ranges[i].device);
+      hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
+      hip_ok(hipMemcpy(all.data() + kTopkRec * i, impl_->topk[i].cand.ptr, kTopkRec, hipMemcpyDeviceToHost),
+             "hipMemcpy");
+    }
+    for (size_t i = 0; i < ns; ++i) {
+      DevGuard g(ranges[i].device);
+      hip_ok(hipMemcpy(impl_->topk[i].all.ptr, all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    }
+  } else if (ns > 1) {
     Comms &cm = comms_for(static_cast<int>(ns));
     std::lock_guard<std::mutex> clk(cm.mu);
     if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
@@ -631,7 +687,7 @@ std::vector<float> run_multi_gpu_jit_host(const HostTable &host, const std::stri
                                           const std::string &cond_cuda) {
   using namespace warpdb;
   const int64_t n = host.num_rows();
-  auto shards = plan_shards(n, device_count());
+  auto shards = plan_shards(n, shard_count());
   // The host result (4 B/row, first-touch bound) is allocated on its own
   // thread while the devices upload and compute; downloads wait for it.
   std::vector<float> result;

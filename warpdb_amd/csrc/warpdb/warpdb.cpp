@@ -207,7 +207,7 @@ warpdb::ResidentShards &WarpDB::shards() {
   if (!shards_) {
     int ndev = 0;
     hip_ok(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
-    if (ndev == 1 && table_.device == 0)
+    if (ndev == 1 && table_.device == 0 && !std::getenv("WARPDB_VIRTUAL_SHARDS"))  // (test hook: multi_gpu.cpp)
       shards_ = warpdb::ResidentShards::borrow(table_);
     else
       shards_ = std::make_unique<warpdb::ResidentShards>(host_table_);
