@@ -21,6 +21,7 @@ from warpdb_amd import _warpexec as wx  # noqa: E402
 D = "WARPDB_EXTRA_DEFINES"
 VARIANTS = {
     "full": {},
+    "lbstats": {D: "WX_RS_DIAG_LBSTATS=1"},
     "no_lookback": {D: "WX_RS_DIAG_NO_LOOKBACK=1"},
     "no_rank": {D: "WX_RS_DIAG_NO_RANK=1"},
     "no_store": {D: "WX_RS_DIAG_NO_STORE=1"},

@@ -2299,6 +2299,12 @@ extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_f_d(WxR
 extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_i_a(WxRadixHistArgs a) { wx_radix_hist_impl<1, true>(a); }
 extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_i_d(WxRadixHistArgs a) { wx_radix_hist_impl<1, false>(a); }
 
+#ifndef WX_RS_DIAG_LBSTATS
+// diagnostic: digit 0's look-back of every tile counts its rounds, sleeps and
+// the predecessors it walked (ctl words 16 + 8 * pass, a 256-B control
+// block); the last tile to finish prints the pass totals
+#define WX_RS_DIAG_LBSTATS 0
+#endif
 #ifndef WX_RS_DIAG_NO_LOOKBACK
 #define WX_RS_DIAG_NO_LOOKBACK 0  // diagnostic: every tile takes its offset as 0 (results invalid)
 #endif
@@ -2533,6 +2539,9 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
       wx_u32 spins = 0;
       wx_u64 t_last = 0ull;  // time of the last progress (0: not yet sampled)
       bool fresh = WX_RS_LB_FIRST;
+#if WX_RS_DIAG_LBSTATS
+      wx_u32 lb_rounds = 0, lb_sleeps = 0;
+#endif
       while (true) {
         wx_u64 wv[WX_RS_LBW];
 #pragma unroll
@@ -2555,6 +2564,9 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
             }
           }
         }
+#if WX_RS_DIAG_LBSTATS
+        ++lb_rounds;
+#endif
         if (done) break;
         if (stop == WX_RS_LBW) {
           p -= WX_RS_LBW;
@@ -2563,6 +2575,9 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
         }
         if (stop > 0) t_last = 0ull;
         p -= stop;
+#if WX_RS_DIAG_LBSTATS
+        ++lb_sleeps;
+#endif
         __builtin_amdgcn_s_sleep(1);
         if ((++spins & 63u) == 0u) {
           // abort only after WX_STALL_TICKS with this digit's chain not moving
@@ -2577,6 +2592,18 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
         }
       }
       wx::st_agent(&row[tid], E | WX_RS_FLAG_P | (excl + tot));
+#if WX_RS_DIAG_LBSTATS
+      if (tid == 0) {
+        wx_u32 *st = a.ctl + 16 + 6 * (a.shift / 8);  // = control word 16 + 8 * pass
+        atomicAdd(&st[0], lb_rounds);
+        atomicAdd(&st[1], lb_sleeps);
+        atomicAdd(&st[2], (wx_u32)((wx_i64)tile - 1 - p));
+        __threadfence();
+        if (atomicAdd(&st[3], 1u) == (wx_u32)((a.n + WX_RS_TILE - 1) / WX_RS_TILE) - 2u)
+          printf("[lbstats] pass %d tiles %u rounds %u sleeps %u walked %u\n", a.shift / 8, atomicAdd(&st[3], 0u) + 1u,
+                 atomicAdd(&st[0], 0u), atomicAdd(&st[1], 0u), atomicAdd(&st[2], 0u));
+      }
+#endif
     }
     S.gb[tid] = a.digit_base[tid] + (wx_u32)excl - ld;
     S.ld[tid] = ld;
