@@ -22,6 +22,11 @@ D = "WARPDB_EXTRA_DEFINES"
 VARIANTS = {
     "full": {},
     "lbstats": {D: "WX_RS_DIAG_LBSTATS=1"},
+    "skip": {D: "WX_RS_SKIP=1"},
+    "skip_m2g2": {D: "WX_RS_SKIP=1,WX_RS_SKIP_MIN=2,WX_RS_SKIP_GROW=2"},
+    "skip_m8g4": {D: "WX_RS_SKIP=1,WX_RS_SKIP_MIN=8,WX_RS_SKIP_GROW=4"},
+    "skip_lbw4": {D: "WX_RS_SKIP=1", "WARPDB_RS_LBW": "4"},
+    "skip_lbstats": {D: "WX_RS_SKIP=1,WX_RS_DIAG_LBSTATS=1"},
     "no_lookback": {D: "WX_RS_DIAG_NO_LOOKBACK=1"},
     "no_rank": {D: "WX_RS_DIAG_NO_RANK=1"},
     "no_store": {D: "WX_RS_DIAG_NO_STORE=1"},
