@@ -22,6 +22,10 @@ D = "WARPDB_EXTRA_DEFINES"
 VARIANTS = {
     "full": {},
     "lbstats": {D: "WX_RS_DIAG_LBSTATS=1"},
+    "full_b": {},
+    "lb_first_b": {D: "WX_RS_LB_FIRST=1"},
+    "full_c": {},
+    "lb_first_c": {D: "WX_RS_LB_FIRST=1"},
     "skip": {D: "WX_RS_SKIP=1"},
     "skip_m2g2": {D: "WX_RS_SKIP=1,WX_RS_SKIP_MIN=2,WX_RS_SKIP_GROW=2"},
     "skip_m8g4": {D: "WX_RS_SKIP=1,WX_RS_SKIP_MIN=8,WX_RS_SKIP_GROW=4"},

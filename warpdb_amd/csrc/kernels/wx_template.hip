@@ -2329,7 +2329,7 @@ extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_i_d(WxR
 #define WX_RS_RANK_LEAD 1  // lane 0's digit group ranked by one ballot, without LDS
 #endif
 #ifndef WX_RS_LB_FIRST
-#define WX_RS_LB_FIRST 0  // load the first predecessor word before the in-tile scan's barrier
+#define WX_RS_LB_FIRST 1  // load the first predecessor word before the in-tile scan's barrier (13.61-13.75 vs 13.83 ms, abl_sort_lbfirst.txt)
 #endif
 #ifndef WX_RS_DIAG_NO_RANK
 #define WX_RS_DIAG_NO_RANK 0  // diagnostic: no in-wave ranking, keys keep their slots (results invalid)
