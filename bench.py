@@ -13,8 +13,10 @@ warpdb_amd.distributed.ShardedQuery, with the exchange each result needs
 (one collective per query):
   project  all-gather of the per-shard passing counts (global placement)
   sum      all-reduce of {sum, count} as two doubles          (C4)
-  group    all-reduce of the 4097-double key window            (C3)
-  topk     all-gather of K packed candidates + merge on the device (C5)
+  group    ONE all-reduce of the key window + per-shard slots of out-of-window
+           groups, merged on the device (wx_group_combine_slots)  (C3)
+  topk     all-gather of one 520-byte candidate record per shard, merged on
+           the device (wx_topk_merge)                             (C5)
   dense    none (WarpDB::query's dense contract, src/warpdb.cpp:243-256)
   sort     single GPU only (ORDER BY without LIMIT: projection + radix sort)
 
@@ -66,6 +68,7 @@ WORKLOADS = {
 # bytes every row reads from HBM (the "HBM-read roofline" of BASELINE.md)
 READ_BYTES = {"project": 8, "dense": 8, "group": 8, "sum": 4, "topk": 4, "sort": 4}
 C4_TOTAL_ROWS = 8e9  # BASELINE.json configs[3]: 8B rows row-sharded over 1/2/4/8 GPUs
+C3_TOTAL_ROWS = 1e9  # BASELINE.json configs[2]: 1B rows, GROUP BY 1K int32 keys (strong-scaled over N GPUs)
 
 
 def parse():
@@ -87,6 +90,12 @@ def parse():
                    help="project only: skip the strong-scaled C4 SUM line (8e9 rows over all GPUs)")
     p.add_argument("--c4-rows", type=float, default=C4_TOTAL_ROWS,
                    help="rows over all GPUs of the C4 SUM line (BASELINE: 8e9)")
+    p.add_argument("--no-c3", action="store_true",
+                   help="project only: skip the strong-scaled C3 GROUP BY line (1e9 rows over all GPUs)")
+    p.add_argument("--c3-rows", type=float, default=C3_TOTAL_ROWS,
+                   help="rows over all GPUs of the strong-scaled C3 GROUP BY line (BASELINE: 1e9)")
+    p.add_argument("--keys", type=int, default=1024,
+                   help="group: distinct int32 keys, uniform over [0, keys) (BASELINE C3: 1K)")
     return p.parse_args()
 
 
@@ -186,7 +195,7 @@ def cpu_leg(args, workload):
 
 
 # ------------------------------------------------------------------ helpers
-def columns_for(workload):
+def columns_for(workload, keys=1024):
     """(name, dtype, seed, kind, lo, hi) of the columns a workload reads."""
     from warpdb_amd import _warpexec as wx
 
@@ -194,7 +203,7 @@ def columns_for(workload):
     if workload in ("sum", "topk", "sort"):
         return [price]
     if workload == "group":
-        return [price, ("quantity", wx.INT32, 3, 1, 0, 1023)]  # 1K int32 groups
+        return [price, ("quantity", wx.INT32, 3, 1, 0, keys - 1)]  # C3: 1K int32 groups
     return [price, ("quantity", wx.FLOAT32, 2, 1, 1, 100)]
 
 
@@ -244,7 +253,18 @@ def _mark(what):
               flush=True)
 
 
-def self_check(workload, sq, cols, n, world, wd, torch, out_v=None):
+def wd_group_doubles(world):
+    from warpdb_amd import _warpexec as wx
+    from warpdb_amd import distributed as wd
+
+    return wx.group_slots_doubles(world, wd.group_slot_groups(world))
+
+
+def group_capacity(keys):
+    return max(4096, keys)
+
+
+def self_check(workload, sq, cols, n, world, wd, torch, out_v=None, keys=1024):
     """One more query after the timed steps, its exchanged result checked
     against torch on each rank's shard (all-reduced): counts and row ids
     exact, float values bit for bit, double sums to 1e-12 relative.  Only
@@ -313,22 +333,28 @@ def self_check(workload, sq, cols, n, world, wd, torch, out_v=None):
             raise SystemExit(f"check failed: SUM {got_s} / {got_c} vs {float(want[0])} / {int(want[1])}")
         return f"ok: count {got_c} exact, sum {got_s:.6e} within 1e-12"
     if workload == "group":
-        keys, sums, counts = sq.group_sum(expr, aux, None, 0, 4096)
+        gk, gs, gc = sq.group_sum(expr, aux, None, 0, group_capacity(keys))
         key = cols["quantity"]
-        ws = torch.zeros(1024, dtype=torch.float64, device="cuda")
-        wc = torch.zeros(1024, dtype=torch.float64, device="cuda")
+        ws = torch.zeros(keys, dtype=torch.float64, device="cuda")
+        wc = torch.zeros(keys, dtype=torch.float64, device="cuda")
         for c0, c1 in chunks():
             kk = key[c0:c1].long()
             ws.index_add_(0, kk, price[c0:c1].double())
             wc.index_add_(0, kk, torch.ones(c1 - c0, dtype=torch.float64, device="cuda"))
-        ws, wc = red(ws).cpu(), red(wc).cpu()
-        present = [g for g in range(1024) if wc[g] > 0]
-        kh, sh, ch = keys.cpu(), sums.cpu(), counts.cpu()
-        if kh.tolist() != present or ch.tolist() != [int(wc[g]) for g in present]:
+        ws, wc = red(ws), red(wc)
+        # present keys in ascending order without a torch select kernel: the
+        # result's keys must index bins holding rows, and their count must be
+        # the number of such bins (keys ascending and inside [0, keys))
+        m = gk.numel()
+        kl = gk.long()
+        ok = m == int((wc > 0).sum()) and (m == 0 or (int(kl[0]) >= 0 and int(kl[-1]) < keys))
+        ok = ok and (m < 2 or bool((kl[1:] > kl[:-1]).all()))
+        if not ok or not torch.equal(gc.double(), wc[kl]):
             raise SystemExit("check failed: GROUP BY keys / counts differ from torch")
-        if any(abs(float(sh[i]) - float(ws[g])) > 1e-12 * abs(float(ws[g])) for i, g in enumerate(present)):
+        rel = (gs - ws[kl]).abs() / ws[kl].abs().clamp_min(1e-300)
+        if m and float(rel.max()) > 1e-12:
             raise SystemExit("check failed: GROUP BY sums differ from torch beyond 1e-12")
-        return f"ok: {len(present)} groups, keys and counts exact, sums within 1e-12"
+        return f"ok: {m} groups, keys and counts exact, sums within 1e-12"
     if workload == "topk":
         tk, ti, tv = sq.topk(expr, None, aux, 5, True)
         # order statistics: the i-th best key t has <= i keys above it and >= i + 1 at or above it
@@ -377,7 +403,7 @@ def main_ranks(args):
     L = wx.make_launch(device=local, stream=stream, custom_src=DISCOUNT_SRC)
     cols = {}
     dmap = {wx.FLOAT32: torch.float32, wx.INT32: torch.int32}
-    for name, dt, seed, kind, lo, hi in columns_for(workload):
+    for name, dt, seed, kind, lo, hi in columns_for(workload, args.keys):
         t = torch.empty(max(1, n), dtype=dmap[dt], device="cuda")[:n]
         wx.fill_synthetic(t.data_ptr(), dt, n, seed, kind, lo, hi, L, row_base=b)
         cols[name] = t
@@ -421,7 +447,12 @@ def main_ranks(args):
             sq.sum_device(expr, aux, res)
     elif workload == "group":
         def step():
-            sq.group_sum_device(expr, aux, None, 0, 4096)
+            if world > 1 and args.keys > wx.GROUP_WINDOW_BINS:
+                # keys beyond the window may outgrow the exchange slots: the
+                # host-checked form, which takes the variable-size merge then
+                sq.group_sum(expr, aux, None, 0, group_capacity(args.keys))
+            else:
+                sq.group_sum_device(expr, aux, None, 0, group_capacity(args.keys))
     else:
         def step():  # results stay in HBM like the other workloads' (no host round trip per query)
             sq.topk_merged_device(expr, None, aux, 5, True)
@@ -466,7 +497,7 @@ def main_ranks(args):
     passing = int(counts.item()) if workload == "project" else None
     mark("check")
     check = None if args.no_check else self_check(workload, sq, cols, n, world, wd, torch,
-                                                  out_v if workload in ("dense", "sort") else None)
+                                                  out_v if workload in ("dense", "sort") else None, keys=args.keys)
     rb = READ_BYTES[workload]
     if workload == "project":
         bytes_per_launch = n * 8 + passing * 8  # 4 B value + 4 B int32 index per passing row
@@ -486,7 +517,9 @@ def main_ranks(args):
                                                for c, t in cols.items()),
                           "index": "int32 shard-local row index" if workload == "project" else None,
                           "exchange": {"project": "all-gather int64 counts", "sum": "all-reduce 2 x f64",
-                                       "group": "all-reduce 4097 x f64 key window", "topk": "all-gather 11 x i64",
+                                       "group": f"one all-reduce of {wd_group_doubles(world)} x f64 (key window + "
+                                                f"{world} slots of out-of-window groups), wx_group_combine_slots",
+                                       "topk": "all-gather 520 B per shard, wx_topk_merge",
                                        "dense": "none", "sort": "none"}[workload] if world > 1 else "none (1 GPU)",
                           "parallelism": f"row-sharded x{world}, one process per GPU"}
         if passing is not None:
@@ -515,7 +548,7 @@ def main_ranks(args):
                     sq2.sum_device(e2, a2, res2)
             else:
                 def step2():
-                    sq2.group_sum_device(e2, a2, None, 0, 4096)
+                    sq2.group_sum_device(e2, a2, None, 0, group_capacity(1024))
             mark(f"secondary {w2}")
             el2, k2_ms, _ = timed(step2)
             chk2 = None if args.no_check else self_check(w2, sq2, cols2, n, world, wd, torch)
@@ -525,7 +558,35 @@ def main_ranks(args):
                              "scaling": line_common(args, world, n_total, el2, w2)["scaling"],
                              "kernel": k2, "kernel_ms": round(k2_ms, 4),
                              "frac": round(b2 / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk2}
-        del qk
+        del qk, sq2
+        # C3 as BASELINE states it, strong-scaled: 1e9 rows (price f32, 1K
+        # int32 keys) over all ranks, 1e9 / N per GPU, each shard generated at
+        # its global row numbers; GROUP BY + the one-collective exchange, so
+        # the driver's 1/2/4/8-GPU runs measure GROUP BY speed-up on a fixed table.
+        if not args.no_c3:
+            c3_total = int(args.c3_rows)
+            b3, e3 = wd.shard_range(c3_total, world, rank)
+            n3 = e3 - b3
+            p3 = torch.empty(max(1, n3), dtype=torch.float32, device="cuda")[:n3]
+            k3 = torch.empty(max(1, n3), dtype=torch.int32, device="cuda")[:n3]
+            wx.fill_synthetic(p3.data_ptr(), wx.FLOAT32, n3, 1, 0, 0.0, 40.0, L, row_base=b3)
+            wx.fill_synthetic(k3.data_ptr(), wx.INT32, n3, 3, 1, 0, 1023, L, row_base=b3)
+            cols3 = {"price": p3, "quantity": k3}
+            sq3 = wd.ShardedQuery(wd.Shard(cols3, b3, n3), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
+            _, e3x, a3x, k3n = WORKLOADS["group"]
+
+            def step3():
+                sq3.group_sum_device(e3x, a3x, None, 0, group_capacity(1024))
+            mark("secondary c3")
+            el3, k3_ms, _ = timed(step3)
+            chk3 = None if args.no_check else self_check("group", sq3, cols3, n3, world, wd, torch)
+            secondary["c3_group_strong"] = {
+                "query": WORKLOADS["group"][0], "config": f"C3: {c3_total:.3g} rows over all GPUs (strong scaling)",
+                "total_rows": c3_total, "rows_per_gpu": n3, "value": round(c3_total * args.steps / el3, 1),
+                "unit": "rows/s", "ms_per_step": round(el3 / args.steps * 1e3, 4), "scaling": "strong",
+                "kernel": k3n, "kernel_ms": round(k3_ms, 4),
+                "frac": round(n3 * READ_BYTES["group"] / (k3_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk3}
+            del p3, k3, sq3, cols3
         # C4 exactly as BASELINE states it: 8e9 rows over all ranks (strong
         # scaling, 8e9 / N per GPU; 32 GB resident at N = 1), SUM + all-reduce,
         # so the driver's 1/2/4/8-GPU runs measure C4's scaling curve.

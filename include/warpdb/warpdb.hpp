@@ -2,6 +2,7 @@
 // include/warpdb.hpp:11-48) running on the MI355X execution layer.
 #pragma once
 #include <memory>
+#include <mutex>
 #include <string>
 #include <utility>
 #include <vector>
@@ -49,9 +50,10 @@ class WarpDB {
   // SUM(expr) WHERE cond over every GPU with an RCCL all-reduce.
   std::pair<double, int64_t> query_multi_gpu_sum(const std::string &expr);
   // "SELECT SUM(v) FROM t [WHERE c] GROUP BY k" over every GPU: per-GPU dense
-  // key-window partials combined by one RCCL all-reduce (keys outside
-  // [key_window_lo, key_window_lo + 2048) merged on the host).  Groups in
-  // ascending key order with double sums and counts (SUM / COUNT / AVG).
+  // key-window partials and per-GPU slots of keys outside [key_window_lo,
+  // key_window_lo + 2048) combined by ONE RCCL all-reduce (more than 64 such
+  // keys on a GPU: merged on the host).  Groups in ascending key order with
+  // double sums and counts: SUM / COUNT / AVG (MIN / MAX are refused).
   warpdb::GroupResult query_multi_gpu_group(const std::string &sql, int32_t key_window_lo = 0);
   // "SELECT e FROM t [WHERE c] ORDER BY o [ASC|DESC] LIMIT k" (k <= 32) over
   // every GPU: K candidates per GPU, one RCCL all-gather, the (key, row) merge.
@@ -73,4 +75,5 @@ class WarpDB {
   Table table_;
   HostTable host_table_;
   std::unique_ptr<warpdb::ResidentShards> shards_;  // query_multi_gpu*: built on first use
+  std::once_flag shards_once_;                      // the bindings release the GIL: one builder
 };

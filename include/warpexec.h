@@ -183,6 +183,46 @@ wx_status wx_group_combine(const double *d_window, int32_t key_window_lo, const 
                            int64_t *d_counts, int64_t *d_n_groups, int64_t *h_n_groups, char *err,
                            size_t errlen);
 
+/* Row-sharded GROUP BY in ONE collective (replaces the
+ * reference's host gather of dense shard results, src/multi_gpu_utils.cpp:23-60).
+ * The exchange buffer holds WX_GROUP_SLOTS_DOUBLES(n_slots, slot_groups)
+ * doubles: the dense window exactly as wx_group_partials writes it, then one
+ * slot per shard of 1 + 3 * slot_groups doubles -- the shard's out-of-window
+ * group count (-1: its general-key table overflowed), then up to slot_groups
+ * (key, sum, count) triples in ascending key order.  wx_group_partials_slots
+ * writes the window, shard `slot`'s slot and zeros in every other slot, so an
+ * element-wise SUM all-reduce of the shards' buffers (one ncclAllReduce,
+ * ncclFloat64) both reduces the window and gathers the slots.  It also writes
+ * ALL of the shard's out-of-window groups to d_keys / d_sums / d_counts
+ * (`capacity` entries) and their count to d_n_extra / h_n_extra, for the
+ * fallback below.  1 <= n_slots <= WX_GROUP_EXCHANGE_MAX_SLOTS, slot_groups >= 1,
+ * n_slots * slot_groups <= 4096. */
+#define WX_GROUP_EXCHANGE_MAX_SLOTS 1024
+#define WX_GROUP_SLOTS_DOUBLES(n_slots, slot_groups) \
+  (WX_GROUP_EXCHANGE_DOUBLES + (int64_t)(n_slots) * (1 + 3 * (int64_t)(slot_groups)))
+#define WX_GROUP_NEEDS_MERGE (-2)
+wx_status wx_group_partials_slots(const wx_table *table, const char *val_expr, const char *key_expr,
+                                  const char *cond, const wx_launch *launch, int32_t key_window_lo,
+                                  double *d_exchange, int32_t n_slots, int32_t slot, int32_t slot_groups,
+                                  int64_t capacity, int32_t *d_keys, double *d_sums, int64_t *d_counts,
+                                  int64_t *d_n_extra, int64_t *h_n_extra, char *err, size_t errlen);
+
+/* The final groups (ascending keys) from a combined exchange buffer
+ * (wx_group_partials_slots layout, summed over the shards): the slots' groups
+ * of equal key are added in slot order, then merged with the window.  The
+ * group count goes to d_n_groups / h_n_groups; it is -1 when a shard's
+ * general-key table overflowed and WX_GROUP_NEEDS_MERGE when some shard had
+ * more than slot_groups out-of-window groups -- every rank reads the same
+ * combined buffer, so every rank sees the same value and can take the
+ * fallback together: a variable-size exchange of the d_keys / d_sums /
+ * d_counts lists of wx_group_partials_slots, then wx_group_combine.  The
+ * kernel never reads the host; a host request over capacity returns
+ * WX_ERR_CAPACITY. */
+wx_status wx_group_combine_slots(const double *d_exchange, int32_t n_slots, int32_t slot_groups,
+                                 int32_t key_window_lo, const wx_launch *launch, int64_t capacity,
+                                 int32_t *d_keys, double *d_sums, int64_t *d_counts, int64_t *d_n_groups,
+                                 int64_t *h_n_groups, char *err, size_t errlen);
+
 /* dst[i] = (dst type) src[i] for i < n, types in wx_dtype numbering (not
  * WX_STRING); C conversion semantics. */
 wx_status wx_cast(const void *d_src, int32_t src_dtype, void *d_dst, int32_t dst_dtype, int64_t n,
@@ -204,6 +244,26 @@ wx_status wx_topk(const wx_table *table, const char *order_expr, const char *con
                   const char *select_expr, int32_t k, int32_t descending,
                   const wx_launch *launch, int64_t row_base, float *d_keys, int64_t *d_idx,
                   float *d_vals, int64_t *d_count, int64_t *h_count, char *err, size_t errlen);
+
+/* One shard's ORDER BY .. LIMIT candidates in the exchange layout (520 bytes):
+ * wx_topk's d_keys / d_vals / d_idx / d_count pointed at keys, vals, rows and
+ * count fill it, so the records of all shards are one all-gather of bytes. */
+typedef struct wx_topk_record {
+  float keys[32];
+  float vals[32];
+  int64_t rows[32]; /* global row numbers (wx_topk's row_base + row) */
+  int64_t count;    /* valid candidates, <= k */
+} wx_topk_record;
+
+/* Global ORDER BY .. LIMIT k of a row-sharded query (the
+ * reference gathers dense shard results on the host, src/multi_gpu_utils.cpp:
+ * 23-60, then sorts them, src/warpdb.cpp:453-455,483-495) from the records
+ * of every shard (device memory, n_records * k <= 4096): better key first (NaN
+ * last, -0.0 == +0.0), ties by the smaller row.  Outputs as wx_topk; the
+ * count (<= k) goes to d_count / h_count.  Runs on the device, no host read. */
+wx_status wx_topk_merge(const wx_topk_record *d_records, int32_t n_records, int32_t k, int32_t descending,
+                        const wx_launch *launch, float *d_keys, int64_t *d_idx, float *d_vals,
+                        int64_t *d_count, int64_t *h_count, char *err, size_t errlen);
 
 /* In-place sorts used by the legacy jit_sort_* entry points.  Stable. */
 wx_status wx_sort_pairs(int32_t *d_keys, float *d_vals, int64_t count, int32_t ascending,

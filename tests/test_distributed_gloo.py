@@ -50,6 +50,73 @@ def group_combine_emulated(win, key_lo, xk, xs, xc):
     return keys[o].astype(np.int32), sums[o], cnts[o]
 
 
+def group_slots_emulated(win, xk, xs, xc, world, rank, slot_groups, n_extra=None):
+    """What wx_group_partials_slots leaves for one shard: the window, then
+    world slots of 1 + 3 * slot_groups doubles -- this shard's count and first
+    slot_groups (key, sum, count) triples, zeros in every other slot."""
+    sl = 1 + 3 * slot_groups
+    slots = np.zeros(world * sl, np.float64)
+    m = len(xk) if n_extra is None else n_extra
+    slots[rank * sl] = m
+    for j in range(min(len(xk), slot_groups)):
+        slots[rank * sl + 1 + 3 * j: rank * sl + 4 + 3 * j] = (xk[j], xs[j], xc[j])
+    return np.concatenate([win, slots])
+
+
+def group_combine_slots_emulated(ex, world, slot_groups, key_lo):
+    """wx_group_combine_slots' contract: -1 / -2 status, else the slots' groups
+    summed per key in slot order and merged with the window (ascending keys)."""
+    W = 2048
+    sl = 1 + 3 * slot_groups
+    slots = ex[2 * W + 1:].reshape(world, sl)
+    cnt = slots[:, 0]
+    if (cnt < 0).any():
+        return -1
+    if (cnt > slot_groups).any():
+        return -2
+    acc = {}
+    for r in range(world):
+        for j in range(int(cnt[r])):
+            k, sm, c = slots[r, 1 + 3 * j: 4 + 3 * j]
+            a = acc.setdefault(int(k), [0.0, 0])
+            a[0] += sm
+            a[1] += int(c)
+    ks = sorted(acc)
+    return group_combine_emulated(ex[:2 * W + 1], key_lo, np.array(ks, np.int32),
+                                  np.array([acc[k][0] for k in ks]), np.array([acc[k][1] for k in ks], np.int64))
+
+
+def topk_record(keys, vals, rows):
+    """One wx_topk_record (include/warpexec.h) as bytes: unused slots junk."""
+    rec = np.zeros(520, np.uint8)
+    kk = np.full(32, np.nan, np.float32); vv = np.full(32, 123.0, np.float32); rr = np.full(32, -7, np.int64)
+    m = len(keys)
+    kk[:m], vv[:m], rr[:m] = keys, vals, rows
+    rec[0:128] = kk.view(np.uint8); rec[128:256] = vv.view(np.uint8); rec[256:512] = rr.view(np.uint8)
+    rec[512:520] = np.array([m], np.int64).view(np.uint8)
+    return rec
+
+
+def topk_merge_emulated(allr, k, desc):
+    """wx_topk_merge's contract over gathered records: better key first (NaN
+    last, -0.0 == +0.0), then the smaller row."""
+    recs = allr.reshape(-1, 520)
+    cand = []
+    for rec in recs:
+        m = int(rec[512:520].view(np.int64)[0])
+        ks, vs, rs = rec[0:128].view(np.float32), rec[128:256].view(np.float32), rec[256:512].view(np.int64)
+        cand += [(ks[j], vs[j], rs[j]) for j in range(m)]
+
+    def order(c):
+        key = float(c[0])
+        return (1 if np.isnan(key) else 0, 0.0 if np.isnan(key) else (-key if desc else key) + 0.0, int(c[2]))
+
+    cand.sort(key=order)
+    cand = cand[:k]
+    return (np.array([c[0] for c in cand], np.float32), np.array([c[2] for c in cand], np.int64),
+            np.array([c[1] for c in cand], np.float32))
+
+
 def _worker(rank: int, world: int, port: int, n: int, errq):
     try:
         sys.path[:0] = [ROOT, HERE]
@@ -108,26 +175,52 @@ def _worker(rank: int, world: int, port: int, n: int, errq):
         wd.exchange_sum_device(out)
         assert int(out[1]) == rc and abs(float(out[0]) - rs) <= 1e-9 * abs(rs)
 
-        # top-K with ties (quantised keys) in both directions
+        # GROUP BY in ONE collective (wx_group_partials_slots layout): the
+        # window all-reduce also gathers every shard's slot of out-of-window
+        # groups; slot sizes 64 (all fit) and 1 (overflow -> the -2 merge path)
+        for key_lo in (0, 512, -5000):
+            win, xk, xs, xc = group_partials_emulated(k, sm, cn, key_lo)
+            for S in (64, 1):
+                ex = torch.from_numpy(group_slots_emulated(win, xk, xs, xc, world, rank, S))
+                wd.all_reduce_(ex)
+                counts = wd.group_slot_counts(ex, world, S)
+                assert wd.group_exchange_error(counts, 1 << 16) is None
+                res = group_combine_slots_emulated(ex.numpy(), world, S, key_lo)
+                if res == -2:  # the fallback: variable-size merge, then the plain combine
+                    assert max(counts) > S
+                    a, b_, c_ = wd.merge_groups(torch.from_numpy(xk), torch.from_numpy(xs), torch.from_numpy(xc),
+                                                counts[rank])
+                    res = group_combine_emulated(ex.numpy()[:2 * 2048 + 1], key_lo, a.numpy(), b_.numpy(), c_.numpy())
+                else:
+                    assert max(counts) <= S
+                ck, cs, cc = res
+                assert np.array_equal(ck, rk) and np.array_equal(cc, rcnt), (key_lo, S)
+                assert np.allclose(cs, rsum, rtol=1e-12, atol=0), (key_lo, S)
+        # an overflow on ONE shard only is seen by every rank in the combined
+        # buffer, so both raise the same error (no rank waits alone in a collective)
+        win, xk, xs, xc = group_partials_emulated(k, sm, cn, 512)
+        bad = {0: None, 1: -1}.get(rank)
+        ex = torch.from_numpy(group_slots_emulated(win, xk, xs, xc, world, rank, 64, n_extra=bad))
+        wd.all_reduce_(ex)
+        errs = wd.group_exchange_error(wd.group_slot_counts(ex, world, 64), 1 << 16)
+        assert errs is not None and "shard 1" in errs, errs
+        cap_small = wd.group_exchange_error(wd.group_slot_counts(
+            torch.from_numpy(group_slots_emulated(win, xk, xs, xc, 1, 0, 64)), 1, 64), 3)
+        assert (cap_small is not None) == (len(xk) > 3)
+
+        # top-K with ties (quantised keys) in both directions: each shard's
+        # wx_topk_record, ONE all-gather of the records, the wx_topk_merge contract
         for desc in (True, False):
             t = {"p": np.floor(synth.uniform_f32(e - b, 1, 0, 40, row_base=b)).astype(np.float32)}
             tk, ti, tv = ora.topk(ora.HostTable(t), "p", 5, desc)
-            mk, mi, mv = wd.merge_topk(torch.from_numpy(tk), torch.from_numpy(ti + b), torch.from_numpy(tv),
-                                       len(tk), 5, desc)
+            rec = torch.from_numpy(topk_record(tk, tv, ti + b))
+            allr = wd.exchange_topk_records(rec)
+            assert allr.numel() == 520 * world
+            mk, mi, mv = topk_merge_emulated(allr.numpy(), 5, desc)
             full = {"p": np.floor(synth.uniform_f32(n, 1, 0, 40)).astype(np.float32)}
             rk2, ri2, _ = ora.topk(ora.HostTable(full), "p", 5, desc)
-            assert np.array_equal(mk.numpy(), rk2) and np.array_equal(mi.numpy(), ri2)
-            # the device-side merge (no host round trip): k slots per shard,
-            # unused ones filled with junk and masked by the shard's count
-            m = len(tk)
-            pk = torch.full((5,), float("nan")); pi = torch.full((5,), -7, dtype=torch.int64)
-            pv = torch.full((5,), 123.0)
-            pk[:m] = torch.from_numpy(tk); pi[:m] = torch.from_numpy(ti + b); pv[:m] = torch.from_numpy(tv)
-            dk, di, dv, dn = wd.merge_topk_device(pk, pi, pv, torch.tensor([m]), 5, desc)
-            c = int(dn[0])
-            assert c == len(rk2)
-            assert np.array_equal(dk[:c].numpy().view(np.uint32), mk.numpy().view(np.uint32))
-            assert np.array_equal(di[:c].numpy(), mi.numpy()) and np.array_equal(dv[:c].numpy(), mv.numpy())
+            assert np.array_equal(mk.view(np.uint32), rk2.view(np.uint32)) and np.array_equal(mi, ri2)
+            assert np.array_equal(mv.view(np.uint32), rk2.view(np.uint32))  # SELECT = the key here
         dist.barrier()
         dist.destroy_process_group()
     except BaseException as ex:  # report to the parent

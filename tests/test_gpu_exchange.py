@@ -1,0 +1,276 @@
+"""GPU tests of the round-3 exchange kernels of the row-sharded path.
+
+* wx_group_partials_slots + an element-wise sum of the shards' buffers (what
+  the ONE all-reduce computes) + wx_group_combine_slots, against the oracle
+  over the whole table: 1..64 shards (views of one table on cuda:0), keys
+  inside and outside the dense window, slots large enough and too small (the
+  -2 status, then the variable-size merge and wx_group_combine), and a
+  shard's general-key table overflow (-1).
+* wx_topk_merge over real per-shard wx_topk records, against the oracle:
+  heavy ties, NaN, +/-0.0, fewer rows than K, both directions, K = 1..32.
+* The multi-rank bench under torchrun with RCCL (the default backend) when
+  more than one GPU is visible -- skipped on a one-GPU box.
+"""
+from __future__ import annotations
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import oracle_lib as ora
+import synth
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+from warpdb_amd import _warpexec as wx  # noqa: E402
+from test_gpu_parity import dev_table, launch, bits  # noqa: E402
+from test_gpu_multi import _shard_views  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+W = wx.GROUP_WINDOW_BINS
+
+
+def _slots_partials(table, world, rank, S, key_lo, cond=None, cap=1 << 14):
+    nd = wx.group_slots_doubles(world, S)
+    ex = torch.full((nd,), float("nan"), dtype=torch.float64, device="cuda")
+    xk = torch.empty(cap, dtype=torch.int32, device="cuda")
+    xs = torch.empty(cap, dtype=torch.float64, device="cuda")
+    xc = torch.empty(cap, dtype=torch.int64, device="cuda")
+    nx = wx.group_partials_slots(table, "price[idx]", "quantity[idx]", cond, launch(), key_lo, ex.data_ptr(), world,
+                                 rank, S, cap, xk.data_ptr(), xs.data_ptr(), xc.data_ptr(), want_count=True)
+    return ex, xk, xs, xc, nx
+
+
+def _combine_slots(ex, world, S, key_lo, cap=1 << 14):
+    ok = torch.empty(cap, dtype=torch.int32, device="cuda")
+    os_ = torch.empty(cap, dtype=torch.float64, device="cuda")
+    oc = torch.empty(cap, dtype=torch.int64, device="cuda")
+    ng = torch.empty(1, dtype=torch.int64, device="cuda")
+    wx.group_combine_slots(ex.data_ptr(), world, S, key_lo, launch(), cap, ok.data_ptr(), os_.data_ptr(),
+                           oc.data_ptr(), d_n_groups=ng.data_ptr())
+    torch.cuda.synchronize()
+    return ok, os_, oc, int(ng.item())
+
+
+@pytest.mark.parametrize("shards,S", [(1, 64), (2, 64), (3, 64), (8, 64), (8, 1), (8, 512), (64, 64), (2, 4096 // 2)])
+@pytest.mark.parametrize("key_lo", [0, 512, -100_000, 900])
+def test_group_slots_match_oracle(shards, S, key_lo):
+    n = 300_007
+    cols = synth.c3_table(n)
+    total = None
+    lists = []
+    sl = 1 + 3 * S
+    for r, (_, t) in enumerate(_shard_views(cols, shards)):
+        if t is None:  # an empty shard still contributes its (zero) buffer
+            t = wx.Table(0, [wx.Column("price", wx.FLOAT32, 0), wx.Column("quantity", wx.INT32, 0)])
+        ex, xk, xs, xc, nx = _slots_partials(t, shards, r, S, key_lo, cond="(price[idx] < 35.0f)")
+        assert not torch.isnan(ex).any()
+        h = ex.cpu().numpy()
+        slots = h[wx.GROUP_EXCHANGE_DOUBLES:].reshape(shards, sl)
+        assert slots[r, 0] == nx and int(h[2 * W]) == nx
+        assert not np.any(np.delete(slots, r, axis=0))  # the other shards' slots are zero
+        m = min(nx, S)  # the slot holds the first S groups, ascending
+        trip = slots[r, 1:1 + 3 * m].reshape(m, 3)
+        assert np.array_equal(trip[:, 0], xk[:m].cpu().numpy()) and np.array_equal(trip[:, 1], xs[:m].cpu().numpy())
+        assert np.array_equal(trip[:, 2], xc[:m].cpu().numpy())
+        total = ex.clone() if total is None else total + ex  # the all-reduce
+        lists.append((xk[:nx], xs[:nx], xc[:nx]))
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", "price < 35")
+    ok, os_, oc, g = _combine_slots(total, shards, S, key_lo)
+    if g == wx.GROUP_NEEDS_MERGE:  # some shard's groups outgrew its slot: the variable-size merge
+        assert max(x[0].numel() for x in lists) > S
+        k = torch.cat([a for a, _, _ in lists]).long()
+        s = torch.cat([b for _, b, _ in lists])
+        c = torch.cat([c for _, _, c in lists])
+        uk, inv = torch.unique(k, sorted=True, return_inverse=True)
+        ms = torch.zeros(uk.numel(), dtype=torch.float64, device="cuda").index_add_(0, inv, s)
+        mc = torch.zeros(uk.numel(), dtype=torch.int64, device="cuda").index_add_(0, inv, c)
+        m = uk.numel()
+        g = wx.group_combine(total.data_ptr(), key_lo, uk.int().contiguous().data_ptr() if m else 0,
+                             ms.data_ptr() if m else 0, mc.data_ptr() if m else 0, m, launch(), 1 << 14,
+                             ok.data_ptr(), os_.data_ptr(), oc.data_ptr(), want_count=True)
+    else:
+        assert max(x[0].numel() for x in lists) <= S
+    assert np.array_equal(ok[:g].cpu().numpy(), rk) and np.array_equal(oc[:g].cpu().numpy(), rc)
+    np.testing.assert_allclose(os_[:g].cpu().numpy(), rs, rtol=1e-12, atol=0)
+    if shards == 1:
+        assert np.array_equal(os_[:g].cpu().numpy(), rs)
+
+
+def test_group_slots_deterministic_and_exact_sum_order():
+    """Equal keys from several slots add in slot order: two combines of the
+    same buffer are bit-identical, and a key present in every slot sums to
+    the slot-order double sum."""
+    world, S = 4, 8
+    nd = wx.group_slots_doubles(world, S)
+    ex = torch.zeros(nd, dtype=torch.float64)
+    sl = 1 + 3 * S
+    vals = [1e16, 1.0, -1e16, 1.0]  # order-sensitive in double
+    for r in range(world):
+        base = wx.GROUP_EXCHANGE_DOUBLES + r * sl
+        ex[base] = 2
+        ex[base + 1: base + 4] = torch.tensor([-7.0, vals[r], 1.0], dtype=torch.float64)
+        ex[base + 4: base + 7] = torch.tensor([5000.0 + r, 2.0, 3.0], dtype=torch.float64)
+    exd = ex.cuda()
+    a = _combine_slots(exd, world, S, 0)
+    b = _combine_slots(exd, world, S, 0)
+    assert a[3] == b[3] == 5
+    assert torch.equal(a[1][:5], b[1][:5])
+    want = ((1e16 + 1.0) + -1e16) + 1.0
+    assert a[0][:5].cpu().tolist() == [-7, 5000, 5001, 5002, 5003]
+    assert a[1][0].item() == want and a[2][0].item() == 4
+    assert a[1][1:5].cpu().tolist() == [2.0] * 4 and a[2][1:5].cpu().tolist() == [3] * 4
+
+
+def test_group_slots_table_overflow_is_minus_one():
+    """More than 4096 distinct out-of-window keys with capacity <= 4096: the
+    shard's table cannot be sorted for the finalize (-1 in its slot), and
+    the combine reports -1 whatever the other slots hold."""
+    n = 20_000
+    cols = {"price": np.ones(n, np.float32), "quantity": (np.arange(n) % 9000).astype(np.int32)}
+    table, _ = dev_table(cols)
+    cap = 4096
+    ex = torch.full((wx.group_slots_doubles(2, 64),), float("nan"), dtype=torch.float64, device="cuda")
+    xk = torch.empty(cap, dtype=torch.int32, device="cuda")
+    xs = torch.empty(cap, dtype=torch.float64, device="cuda")
+    xc = torch.empty(cap, dtype=torch.int64, device="cuda")
+    wx.group_partials_slots(table, "price[idx]", "quantity[idx]", None, launch(0), 0, ex.data_ptr(), 2, 1, 64, cap,
+                            xk.data_ptr(), xs.data_ptr(), xc.data_ptr())  # asynchronous: no error raised here
+    with pytest.raises(wx.WarpExecError) as e:  # the shard's own flag, reported (and cleared) by the check
+        wx.check(launch())
+    assert e.value.status == wx.WX_ERR_UNSUPPORTED
+    h = ex.cpu().numpy()
+    assert h[wx.GROUP_EXCHANGE_DOUBLES + (1 + 3 * 64)] == -1.0
+    assert _combine_slots(ex, 2, 64, 0)[3] == -1
+
+
+def test_group_slots_bad_arguments():
+    ex = torch.zeros(wx.group_slots_doubles(2, 64), dtype=torch.float64, device="cuda")
+    for world, S in ((0, 64), (2, 0), (2, 4096), (2000, 1)):
+        with pytest.raises(wx.WarpExecError) as e:
+            wx.group_combine_slots(ex.data_ptr(), world, S, 0, launch(), 0, 0, 0, 0)
+        assert e.value.status == wx.WX_ERR_INVALID
+
+
+def _records(host, shards, k, desc, cond=None, select=None):
+    """Each shard's real wx_topk output written into its wx_topk_record."""
+    n = len(next(iter(host.values())))
+    views = _shard_views(host, shards)
+    recs = torch.zeros(shards * wx.TOPK_RECORD_BYTES, dtype=torch.uint8, device="cuda")
+    for r, (b, t) in enumerate(views):
+        rec = recs[r * wx.TOPK_RECORD_BYTES:(r + 1) * wx.TOPK_RECORD_BYTES]
+        rec[:128].view(torch.float32).fill_(float("nan"))  # junk beyond the count
+        rec[256:512].view(torch.int64).fill_(-5)
+        if t is None:
+            continue
+        wx.topk(t, "price[idx]", cond, select, k, desc, launch(), rec[:128].data_ptr(), rec[256:512].data_ptr(),
+                rec[128:256].data_ptr(), row_base=b, d_count=rec[512:520].data_ptr(), want_count=False)
+    torch.cuda.synchronize()
+    assert n >= 0
+    return recs
+
+
+@pytest.mark.parametrize("rows", [3, 1000, 300_007])
+@pytest.mark.parametrize("shards", [1, 2, 3, 8, 128])
+@pytest.mark.parametrize("k,desc", [(5, True), (5, False), (32, True), (1, False)])
+def test_topk_merge_matches_oracle(rows, shards, k, desc):
+    if shards * k > wx.TOPK_MERGE_MAX:
+        pytest.skip("n_records * k above the merge bound")
+    i = np.arange(rows)
+    price = ((i // 7) % 13).astype(np.float32) - 6.0  # heavy ties
+    price[i % 97 == 5] = np.nan
+    price[i % 89 == 3] = -0.0
+    qty = (i % 5).astype(np.float32)
+    host = {"price": price, "quantity": qty}
+    recs = _records(host, shards, k, desc, cond="(quantity[idx] > 0.0f)", select="(price[idx] * quantity[idx])")
+    out_k = torch.empty(k, dtype=torch.float32, device="cuda")
+    out_i = torch.empty(k, dtype=torch.int64, device="cuda")
+    out_v = torch.empty(k, dtype=torch.float32, device="cuda")
+    cnt = wx.topk_merge(recs.data_ptr(), shards, k, desc, launch(), out_k.data_ptr(), out_i.data_ptr(),
+                        out_v.data_ptr(), want_count=True)
+    ok_, oi, ov = ora.topk(ora.HostTable(host), "price", k, desc, cond="quantity > 0", select_expr="price * quantity")
+    assert cnt == len(oi)
+    assert np.array_equal(out_i[:cnt].cpu().numpy(), oi)
+    assert np.array_equal(bits(out_k[:cnt].cpu().numpy()), bits(ok_))
+    assert np.array_equal(bits(out_v[:cnt].cpu().numpy()), bits(ov))
+
+
+def test_topk_merge_bounds():
+    recs = torch.zeros(wx.TOPK_RECORD_BYTES * 200, dtype=torch.uint8, device="cuda")
+    with pytest.raises(wx.WarpExecError) as e:
+        wx.topk_merge(recs.data_ptr(), 200, 32, True, launch())
+    assert e.value.status == wx.WX_ERR_UNSUPPORTED
+    with pytest.raises(wx.WarpExecError):
+        wx.topk_merge(recs.data_ptr(), 2, 33, True, launch())
+    assert wx.topk_merge(recs.data_ptr(), 0, 5, True, launch(), want_count=True) == 0
+
+
+# ------------------------------------------- RCCL: one process per GPU (>= 2 GPUs)
+def _ngpus():
+    return torch.cuda.device_count()
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="one GPU visible: the RCCL runs need a multi-GPU box")
+@pytest.mark.parametrize("workload,extra", [
+    ("project", ["--rows", "2e7", "--c4-rows", "40000001"]),
+    ("sum", ["--total-rows", "40000001"]),
+    ("group", ["--rows", "1e7"]),
+    ("group", ["--total-rows", "2e7"]),
+    ("topk", ["--rows", "1e7"]),
+])
+def test_bench_rccl_ranks(workload, extra):
+    """bench.py under torchrun with the default (RCCL) backend, one rank per
+    visible GPU (at most 8): the product's exchanges over xGMI, each line's
+    own result check."""
+    n = min(8, _ngpus())
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    env = {k: v for k, v in os.environ.items() if k != "WARPDB_DIST_BACKEND"}
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
+                        "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
+                        "--gpus", str(n), "--workload", workload, "--steps", "3", "--warmup", "1",
+                        "--no-cpu-baseline", *extra],
+                       capture_output=True, text=True, cwd=ROOT, env=env, timeout=600)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    assert d["n_gpus"] == n and d["value"] > 0 and str(d["check"]).startswith("ok"), d
+    for v in (d.get("secondary") or {}).values():
+        assert str(v["check"]).startswith("ok"), v
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="one GPU visible: the RCCL runs need a multi-GPU box")
+def test_warpdb_multi_gpu_all_devices_against_oracle(tmp_path):
+    """WarpDB::query_multi_gpu{,_sum,_group,_topk} over every visible GPU
+    (ncclCommInitAll, one thread + stream per device) against the oracle."""
+    from warpdb_amd import pywarpdb as pw
+
+    m = 200_003
+    small = synth.c2_table(m)
+    small["quantity"] = small["quantity"].astype(np.float32)
+    path = tmp_path / "t.csv"
+    with open(path, "w") as f:
+        f.write("price,quantity\n")
+        for p_, q_ in zip(small["price"].tolist(), small["quantity"].tolist()):
+            f.write(f"{p_!r},{q_!r}\n")
+    db = pw.WarpDB(str(path))
+    hs = ora.HostTable(small)
+    r = np.asarray(db.query_multi_gpu("price * quantity WHERE price > 15"), np.float32)
+    assert np.array_equal(bits(r), bits(ora.dense(hs, "price * quantity", "price > 15", np.zeros(m, np.float32))))
+    s2, c2 = db.query_multi_gpu_sum("price * 0.9 WHERE price > 20")
+    es2, ec2 = ora.reduce_sum(hs, "price * 0.9", "price > 20")
+    assert c2 == ec2 and abs(s2 - es2) <= 1e-12 * abs(es2)
+    for sql, lo in (("SELECT SUM(price) FROM t GROUP BY quantity", 0),):
+        k, s, c = db.query_multi_gpu_group(sql)
+        rk, rs, rc = ora.group_sum(hs, "price", "quantity")
+        assert np.array_equal(k, rk) and np.array_equal(c, rc)
+        np.testing.assert_allclose(s, rs, rtol=1e-12, atol=0)
+    k2, rows2, v2 = db.query_multi_gpu_topk("SELECT price FROM t ORDER BY price DESC LIMIT 7")
+    ok2, oi2, ov2 = ora.topk(hs, "price", 7, True, select_expr="price")
+    assert np.array_equal(rows2, oi2) and np.array_equal(bits(v2), bits(ov2))

@@ -322,7 +322,8 @@ def test_two_threads_share_one_warpdb():
 
 
 @pytest.mark.parametrize("args", [
-    ["--workload", "project", "--c4-rows", "3000001"], ["--workload", "sum", "--total-rows", "3000001"], ["--workload", "group"],
+    ["--workload", "project", "--c4-rows", "3000001", "--c3-rows", "2000001"],
+    ["--workload", "group", "--keys", "300000"], ["--workload", "sum", "--total-rows", "3000001"], ["--workload", "group"],
     ["--workload", "topk"], ["--workload", "dense"], ["--workload", "sort"],
     ["--workload", "sum", "--api", "--total-rows", "3000001"], ["--workload", "group", "--api"],
     ["--workload", "topk", "--api"]])
@@ -341,9 +342,10 @@ def test_bench_json_contract(args):
         assert str(line["check"]).startswith("ok"), line["check"]
     if args[1] == "project":  # SUM, GROUP BY and C4's strong-scaled SUM measured beside the headline
         sec = line["secondary"]
-        assert set(sec) == {"sum", "group", "c4_sum_strong"}, sec
+        assert set(sec) == {"sum", "group", "c3_group_strong", "c4_sum_strong"}, sec
         assert all(str(v["check"]).startswith("ok") and v["value"] > 0 for v in sec.values()), sec
         assert sec["c4_sum_strong"]["total_rows"] == 3000001 and sec["c4_sum_strong"]["scaling"] == "strong"
+        assert sec["c3_group_strong"]["total_rows"] == 2000001 and sec["c3_group_strong"]["scaling"] == "strong"
 
 
 @pytest.mark.parametrize("nshards", [2, 3])

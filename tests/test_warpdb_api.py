@@ -248,9 +248,10 @@ def test_sharded_query_single_rank():
 
 
 @pytest.mark.parametrize("workload,extra", [
-    ("project", ["--rows", "1e7", "--c4-rows", "20000001"]),
+    ("project", ["--rows", "1e7", "--c4-rows", "20000001", "--c3-rows", "10000001"]),
     ("sum", ["--total-rows", "20000001"]),  # C4's strong-scaling form, ragged shards
-    ("group", ["--rows", "5e6"]),           # the dense-window all-reduce
+    ("group", ["--rows", "5e6"]),           # the one-collective window + slots all-reduce
+    ("group", ["--rows", "2e6", "--keys", "3000"]),  # keys outside the window ride in the slots / the merge
     ("topk", ["--rows", "5e6"]),
 ])
 def test_bench_two_ranks_on_one_gpu(workload, extra):
@@ -280,6 +281,8 @@ def test_bench_two_ranks_on_one_gpu(workload, extra):
         assert d["config"]["passing_rows_per_gpu"] > 0.6 * 10**7
         c4 = d["secondary"]["c4_sum_strong"]  # C4's strong-scaled SUM beside the headline
         assert c4["total_rows"] == 20000001 and c4["rows_per_gpu"] == 10000001 and str(c4["check"]).startswith("ok")
+        c3 = d["secondary"]["c3_group_strong"]  # C3's strong-scaled GROUP BY beside it
+        assert c3["total_rows"] == 10000001 and c3["rows_per_gpu"] == 5000001 and str(c3["check"]).startswith("ok")
     if workload == "sum":
         assert d["config"]["total_rows"] == 20000001 and d["scaling"] == "strong"
         assert d["config"]["rows_per_gpu"] == 10000001

@@ -36,6 +36,17 @@ F_F64_COUNTS = 8  # reduce_sum: count written as a double (one f64 all-reduce co
 
 GROUP_WINDOW_BINS = 2048
 GROUP_EXCHANGE_DOUBLES = 2 * GROUP_WINDOW_BINS + 1  # [sums | counts as f64 | out-of-window groups]
+GROUP_EXCHANGE_MAX_SLOTS = 1024
+GROUP_SLOT_MAX = 4096  # n_slots * slot_groups bound
+GROUP_NEEDS_MERGE = -2  # wx_group_combine_slots: some shard's out-of-window groups did not fit its slot
+TOPK_MAX = 32
+TOPK_RECORD_BYTES = TOPK_MAX * 16 + 8  # wx_topk_record: keys f32[32] | vals f32[32] | rows i64[32] | count i64
+TOPK_MERGE_MAX = 4096  # n_records * k bound
+
+
+def group_slots_doubles(n_slots: int, slot_groups: int) -> int:
+    """WX_GROUP_SLOTS_DOUBLES: the one-collective GROUP BY exchange buffer."""
+    return GROUP_EXCHANGE_DOUBLES + n_slots * (1 + 3 * slot_groups)
 
 MODE_DENSE = 0
 MODE_DENSE_FILL = 1
@@ -51,6 +62,9 @@ EXPORTED_SYMBOLS = (
     "wx_group_agg",
     "wx_group_partials",
     "wx_group_combine",
+    "wx_group_partials_slots",
+    "wx_group_combine_slots",
+    "wx_topk_merge",
     "wx_cast",
     "wx_topk",
     "wx_sort_pairs",
@@ -126,6 +140,9 @@ def load() -> ctypes.CDLL:
         "wx_group_agg": [T, E, E, E, L, I32, I64, P, P, P, P, P, P, pI64, E, S],
         "wx_group_partials": [T, E, E, E, L, I32, P, I64, P, P, P, P, pI64, E, S],
         "wx_group_combine": [P, I32, P, P, P, I64, L, I64, P, P, P, P, pI64, E, S],
+        "wx_group_partials_slots": [T, E, E, E, L, I32, P, I32, I32, I32, I64, P, P, P, P, pI64, E, S],
+        "wx_group_combine_slots": [P, I32, I32, I32, L, I64, P, P, P, P, pI64, E, S],
+        "wx_topk_merge": [P, I32, I32, I32, L, P, P, P, P, pI64, E, S],
         "wx_cast": [P, I32, P, I32, I64, L, E, S],
         "wx_topk": [T, E, E, E, I32, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_sort_pairs": [P, P, I64, I32, L, E, S],
@@ -301,6 +318,52 @@ def group_combine(d_window: int, key_window_lo: int, d_x_keys: int, d_x_sums: in
                               n_extra, ctypes.byref(launch), capacity, d_keys or None, d_sums or None,
                               d_counts or None, d_n_groups or None, ctypes.byref(h) if want_count else None,
                               err, len(err))
+    _check(st, err)
+    return h.value if want_count else None
+
+
+def group_partials_slots(table: Table, val_expr: str, key_expr: str, cond: Optional[str], launch: WxLaunch,
+                         key_window_lo: int, d_exchange: int, n_slots: int, slot: int, slot_groups: int,
+                         capacity: int, d_keys: int, d_sums: int, d_counts: int, d_n_extra: int = 0,
+                         want_count: bool = False) -> Optional[int]:
+    """Per-shard GROUP BY partials in the one-collective exchange layout
+    (window + this shard's slot, zeros in the others; include/warpexec.h)."""
+    lib = load()
+    err = _err()
+    h = ctypes.c_int64(-1)
+    st = lib.wx_group_partials_slots(ctypes.byref(table.c), _enc(val_expr), _enc(key_expr), _enc(cond),
+                                     ctypes.byref(launch), key_window_lo, d_exchange, n_slots, slot, slot_groups,
+                                     capacity, d_keys or None, d_sums or None, d_counts or None, d_n_extra or None,
+                                     ctypes.byref(h) if want_count else None, err, len(err))
+    _check(st, err)
+    return h.value if want_count else None
+
+
+def group_combine_slots(d_exchange: int, n_slots: int, slot_groups: int, key_window_lo: int, launch: WxLaunch,
+                        capacity: int, d_keys: int, d_sums: int, d_counts: int, d_n_groups: int = 0,
+                        want_count: bool = False) -> Optional[int]:
+    """Final groups from a combined one-collective exchange buffer; the count
+    is GROUP_NEEDS_MERGE (-2) when a shard's slot overflowed, -1 when a
+    shard's general-key table did."""
+    lib = load()
+    err = _err()
+    h = ctypes.c_int64(-1)
+    st = lib.wx_group_combine_slots(d_exchange, n_slots, slot_groups, key_window_lo, ctypes.byref(launch), capacity,
+                                    d_keys or None, d_sums or None, d_counts or None, d_n_groups or None,
+                                    ctypes.byref(h) if want_count else None, err, len(err))
+    _check(st, err)
+    return h.value if want_count else None
+
+
+def topk_merge(d_records: int, n_records: int, k: int, descending: bool, launch: WxLaunch, d_keys: int = 0,
+               d_idx: int = 0, d_vals: int = 0, d_count: int = 0, want_count: bool = False) -> Optional[int]:
+    """Global top-K from n_records wx_topk_record candidate records (device)."""
+    lib = load()
+    err = _err()
+    h = ctypes.c_int64(-1)
+    st = lib.wx_topk_merge(d_records or None, n_records, k, 1 if descending else 0, ctypes.byref(launch),
+                           d_keys or None, d_idx or None, d_vals or None, d_count or None,
+                           ctypes.byref(h) if want_count else None, err, len(err))
     _check(st, err)
     return h.value if want_count else None
 

@@ -124,10 +124,50 @@ struct WxGroupFinArgs {
   // as [W sums | W counts as f64 | 1 out-of-window group count], and only the
   // out-of-window groups go to out_keys / out_sums / out_counts
   double *win_out;
+  // nullable (partials mode): the one-collective exchange slots that follow
+  // the window -- n_slots x (1 + 3 * slot_groups) doubles; this shard writes
+  // its own slot (count, then (key, sum, count) triples) and zeros the others
+  double *slots;
+  int n_slots;
+  int slot_rank;
+  int slot_groups;
+};
+
+// Slot layout of the one-collective GROUP BY exchange (wx_group_partials_slots)
+#define WX_GROUP_EXCHANGE (2 * WX_GROUP_WINDOW + 1)
+#define WX_GROUP_SLOT_MAX 4096  // n_slots * slot_groups bound (the merge sorts them in LDS)
+
+// Final GROUP BY result from a combined one-collective exchange buffer: the
+// window and every shard's slot of out-of-window groups.
+struct WxGroupSlotsArgs {
+  const double *exchange;  // [WX_GROUP_EXCHANGE + n_slots * (1 + 3 * slot_groups)]
+  int n_slots;
+  int slot_groups;
+  int key_lo;
+  int *out_keys;
+  double *out_sums;
+  wx_i64 *out_counts;
+  wx_i64 capacity;
+  wx_i64 *n_groups_out;  // -1: a shard's general-key table overflowed; -2: a slot overflowed (merge needed)
+};
+
+// Top-K exchange record of one shard (wx_topk_record in warpexec.h)
+#define WX_TOPK_REC_BYTES (WX_TOPK_MAX * 16 + 8)
+#define WX_TOPK_MERGE_MAX 4096  // n_records * k bound
+
+struct WxTopkMergeArgs {
+  const unsigned char *records;  // n_records x WX_TOPK_REC_BYTES
+  int n_records;
+  int k;
+  int descending;
+  float *out_keys;
+  wx_i64 *out_idx;
+  float *out_vals;
+  wx_i64 *count_out;
 };
 
 // Final GROUP BY result from a combined exchange window (wx_group_partials
-// layout) and the combined out-of-window groups (ascending keys).
+// layout) and the combined out-of-window groups (ascending keys, unique).
 struct WxGroupCombineArgs {
   const double *window;  // [2 * WX_GROUP_WINDOW + 1]
   const int *x_keys;     // [n_extra], ascending, none inside the window

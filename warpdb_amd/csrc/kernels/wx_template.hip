@@ -1565,6 +1565,33 @@ extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(Wx
 #endif
     }
   }
+  // one-collective exchange slots (partials mode): this shard's slot holds
+  // its out-of-window group count (-1: table overflow) and the first
+  // slot_groups of those groups, ascending (they sit at positions 0..nh of
+  // the key order here); every other shard's slot is zero, so a SUM
+  // all-reduce of the shards' buffers gathers the slots
+  if (part && a.slots) {
+    const int sl = 1 + 3 * a.slot_groups;
+    const int nd = a.n_slots * sl;
+    for (int q = tid; q < nd; q += WX_GFIN_BLOCK) {
+      const int r = q / sl, o = q - r * sl;
+      double v = 0.0;
+      if (r == a.slot_rank) {
+        if (o == 0) {
+          v = too_many ? -1.0 : (double)nh;
+        } else {
+          const int j = (o - 1) / 3, fld = (o - 1) - 3 * j;
+          if (j < nh) {
+            const wx_u64 e = WX_ENT(j);
+            const wx_u32 slot = a.h_used[(wx_u32)e];
+            v = fld == 0 ? (double)(int)((wx_u32)(e >> 32) ^ 0x80000000u)
+                         : (fld == 1 ? a.h_sum[slot] : (double)a.h_cnt[slot]);
+          }
+        }
+      }
+      a.slots[q] = v;
+    }
+  }
   __syncthreads();
   const wx_i64 total = out_pos + (nh - nlo);
   // return the general-key table to its clean state
@@ -1945,9 +1972,8 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_fill_synthetic(WxFillA
 // wx_group_finalize).
 #define WX_GCOMB_BLOCK 1024
 static_assert(WX_GROUP_WINDOW == 2 * WX_GCOMB_BLOCK, "two window bins per combine thread");
-extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine(WxGroupCombineArgs a) {
-  __shared__ wx_u32 s_wtot[WX_GCOMB_BLOCK / 64];
-  __shared__ wx_i64 s_nlo;
+// x_keys / x_sums / x_counts: global or LDS (flat pointers)
+__device__ __forceinline__ void wx_group_combine_body(const WxGroupCombineArgs &a, wx_u32 *s_wtot, wx_i64 *s_nlo) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int b0 = 2 * tid;
   const double c0 = a.window[WX_GROUP_WINDOW + b0], c1 = a.window[WX_GROUP_WINDOW + b0 + 1];
@@ -1958,7 +1984,7 @@ extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine(Wx
       if (a.x_keys[mid] < a.key_lo) lo = mid + 1;
       else hi = mid;
     }
-    s_nlo = lo;
+    *s_nlo = lo;
   }
   const wx_u32 f = (c0 != 0.0 ? 1u : 0u) + (c1 != 0.0 ? 1u : 0u);
   wx_u32 incl = f;
@@ -1976,7 +2002,7 @@ extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine(Wx
     wbase += (w < wave) ? v : 0u;
     wsum += v;
   }
-  const wx_i64 nlo = s_nlo;
+  const wx_i64 nlo = *s_nlo;
   wx_i64 pos = nlo + wbase + incl - f;
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -2000,6 +2026,208 @@ extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine(Wx
     }
   }
   if (tid == 0) *a.n_groups_out = above + (a.n_extra - nlo);
+}
+
+extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine(WxGroupCombineArgs a) {
+  __shared__ wx_u32 s_wtot[WX_GCOMB_BLOCK / 64];
+  __shared__ wx_i64 s_nlo;
+  wx_group_combine_body(a, s_wtot, &s_nlo);
+}
+
+// The one-collective form (wx_group_combine_slots): the exchange buffer is
+// the window followed by one slot per shard (count, then (key, sum, count)
+// triples, ascending keys).  The slots' groups are sorted in LDS by (key,
+// slot), groups of equal key are summed in slot order (so every rank and
+// every run adds them in the same order), and the unique groups are merged
+// with the window exactly as wx_group_combine does.  A slot whose shard had
+// more out-of-window groups than fit (count > slot_groups) makes the result
+// -2: the caller merges those groups with a variable-size exchange instead.
+extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine_slots(WxGroupSlotsArgs a) {
+  __shared__ wx_u64 s_ent[WX_GROUP_SLOT_MAX];  // (key ^ sign) << 32 | slot-major entry index
+  __shared__ int s_key[WX_GROUP_SLOT_MAX];
+  __shared__ double s_sum[WX_GROUP_SLOT_MAX];
+  __shared__ wx_i64 s_cnt[WX_GROUP_SLOT_MAX];
+  __shared__ int s_off[WX_GCOMB_BLOCK + 1];  // entry offset of each slot (n_slots <= WX_GCOMB_BLOCK)
+  __shared__ wx_u32 s_wtot[WX_GCOMB_BLOCK / 64];
+  __shared__ wx_i64 s_nlo;
+  __shared__ int s_state;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sl = 1 + 3 * a.slot_groups;
+  const double *slots = a.exchange + WX_GROUP_EXCHANGE;
+  if (tid == 0) s_state = 0;
+  {  // slot counts (thread r: slot r), their prefix by a block scan
+    const double c = tid < a.n_slots ? slots[(wx_i64)tid * sl] : 0.0;
+    __syncthreads();
+    if (c < 0.0) atomicMax(&s_state, 2);
+    else if (c > (double)a.slot_groups) atomicMax(&s_state, 1);
+    const wx_u32 mine = (c > 0.0 && c <= (double)a.slot_groups) ? (wx_u32)c : 0u;
+    wx_u32 incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_u32 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_wtot[wave] = incl;
+    __syncthreads();
+    wx_u32 base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WX_GCOMB_BLOCK / 64; ++w) {
+      const wx_u32 v = s_wtot[w];
+      base += (w < wave) ? v : 0u;
+      tot += v;
+    }
+    s_off[tid] = (int)(base + incl - mine);
+    if (tid == 0) s_off[a.n_slots] = (int)tot;
+    __syncthreads();
+  }
+  if (s_state != 0) {
+    if (tid == 0) *a.n_groups_out = s_state == 2 ? -1 : -2;
+    return;
+  }
+  const int T = s_off[a.n_slots];
+  int npad = 1;
+  while (npad < T) npad <<= 1;
+  for (int i = tid; i < npad; i += WX_GCOMB_BLOCK) {
+    wx_u64 e = ~0ull;
+    if (i < T) {
+      int lo = 0, hi = a.n_slots - 1;  // the slot holding entry i: last r with s_off[r] <= i
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= i) lo = mid;
+        else hi = mid - 1;
+      }
+      const int j = i - s_off[lo];
+      const int key = (int)slots[(wx_i64)lo * sl + 1 + 3 * j];
+      e = ((wx_u64)((wx_u32)key ^ 0x80000000u) << 32) | ((wx_u32)lo * (wx_u32)a.slot_groups + (wx_u32)j);
+    }
+    s_ent[i] = e;
+  }
+  __syncthreads();
+  for (int k = 2; k <= npad; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < npad; i += WX_GCOMB_BLOCK) {
+        const int p = i ^ j;
+        if (p > i) {
+          const wx_u64 x = s_ent[i], y = s_ent[p];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) { s_ent[i] = y; s_ent[p] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  // unique keys: run heads ranked by a block scan (4 consecutive entries per thread)
+  constexpr int PER = WX_GROUP_SLOT_MAX / WX_GCOMB_BLOCK;
+  wx_u32 hm = 0u, nh = 0u;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = tid * PER + q;
+    if (i < T && (i == 0 || (s_ent[i] >> 32) != (s_ent[i - 1] >> 32))) { hm |= 1u << q; ++nh; }
+  }
+  wx_u32 incl = nh;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const wx_u32 t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_wtot[wave] = incl;
+  __syncthreads();
+  wx_u32 wbase = 0, usum = 0;
+#pragma unroll
+  for (int w = 0; w < WX_GCOMB_BLOCK / 64; ++w) {
+    const wx_u32 v = s_wtot[w];
+    wbase += (w < wave) ? v : 0u;
+    usum += v;
+  }
+  wx_u32 u = wbase + incl - nh;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (!(hm & (1u << q))) continue;
+    const int i0 = tid * PER + q;
+    const wx_u32 kk = (wx_u32)(s_ent[i0] >> 32);
+    double sum = 0.0;
+    wx_i64 cnt = 0;
+    for (int i = i0; i < T && (wx_u32)(s_ent[i] >> 32) == kk; ++i) {  // slot order
+      const wx_u32 ent = (wx_u32)s_ent[i];
+      const int r = (int)(ent / (wx_u32)a.slot_groups), j = (int)(ent % (wx_u32)a.slot_groups);
+      const double *g = slots + (wx_i64)r * sl + 1 + 3 * j;
+      sum += g[1];
+      cnt += (wx_i64)g[2];
+    }
+    s_key[u] = (int)(kk ^ 0x80000000u);
+    s_sum[u] = sum;
+    s_cnt[u] = cnt;
+    ++u;
+  }
+  __syncthreads();
+  WxGroupCombineArgs c;
+  c.window = a.exchange;
+  c.x_keys = s_key;
+  c.x_sums = s_sum;
+  c.x_counts = s_cnt;
+  c.n_extra = usum;
+  c.key_lo = a.key_lo;
+  c.out_keys = a.out_keys;
+  c.out_sums = a.out_sums;
+  c.out_counts = a.out_counts;
+  c.capacity = a.capacity;
+  c.n_groups_out = a.n_groups_out;
+  wx_group_combine_body(c, s_wtot + 0, &s_nlo);
+}
+
+// Global ORDER BY .. LIMIT k of a row-sharded query from every shard's
+// candidates (wx_topk_merge): n_records records of <= k (key, value, row)
+// candidates each.  A candidate's place is the number of candidates that
+// beat it in the total order (better key -- NaN last, -0.0 == +0.0 -- then
+// the smaller row, then the earlier candidate), counted over all of them in
+// LDS; places < k are written.  n_records * k <= WX_TOPK_MERGE_MAX.
+extern "C" __global__ __launch_bounds__(1024) void wx_topk_merge(WxTopkMergeArgs a) {
+  __shared__ wx_u32 s_r[WX_TOPK_MERGE_MAX];
+  __shared__ wx_i64 s_row[WX_TOPK_MERGE_MAX];
+  __shared__ int s_src[WX_TOPK_MERGE_MAX];  // record * 32 + slot, or -1 for an unused slot
+  __shared__ int s_tot;
+  const int tid = threadIdx.x;
+  const int nc = a.n_records * a.k;
+  for (int c = tid; c < nc; c += 1024) {
+    const int r = c / a.k, j = c - r * a.k;
+    const unsigned char *rec = a.records + (wx_i64)r * WX_TOPK_REC_BYTES;
+    const wx_i64 m = *reinterpret_cast<const wx_i64 *>(rec + WX_TOPK_MAX * 16);
+    if (j < m) {
+      const float key = reinterpret_cast<const float *>(rec)[j];
+      const wx_u32 o = wx::f2ord(key);
+      s_r[c] = (a.descending || o == 0u) ? o : ~o;  // larger is better; NaN (0) worst
+      s_row[c] = reinterpret_cast<const wx_i64 *>(rec + WX_TOPK_MAX * 8)[j];
+      s_src[c] = r * WX_TOPK_MAX + j;
+    } else {
+      s_r[c] = 0u;
+      s_row[c] = 0;
+      s_src[c] = -1;
+    }
+  }
+  if (tid == 0) s_tot = 0;
+  __syncthreads();
+  for (int c = tid; c < nc; c += 1024) {
+    const int src = s_src[c];
+    if (src < 0) continue;
+    atomicAdd(&s_tot, 1);
+    const wx_u32 rc = s_r[c];
+    const wx_i64 wc = s_row[c];
+    int place = 0;
+    for (int d = 0; d < nc; ++d) {
+      if (s_src[d] < 0 || d == c) continue;
+      const wx_u32 rd = s_r[d];
+      const wx_i64 wd = s_row[d];
+      place += (rd > rc || (rd == rc && (wd < wc || (wd == wc && d < c)))) ? 1 : 0;
+    }
+    if (place < a.k) {
+      const unsigned char *rec = a.records + (wx_i64)(src / WX_TOPK_MAX) * WX_TOPK_REC_BYTES;
+      const int j = src % WX_TOPK_MAX;
+      if (a.out_keys) a.out_keys[place] = reinterpret_cast<const float *>(rec)[j];
+      if (a.out_vals) a.out_vals[place] = reinterpret_cast<const float *>(rec + WX_TOPK_MAX * 4)[j];
+      if (a.out_idx) a.out_idx[place] = wc;
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && a.count_out) *a.count_out = s_tot < a.k ? s_tot : a.k;
 }
 
 // Element-wise C conversion between the column types (wx_cast), e.g. the

@@ -5,8 +5,9 @@
 // and downloads its slice of the result, so the devices run concurrently.
 // The cross-device exchanges are the aggregates' (SURVEY.md 8(e)), each ONE
 // RCCL all-reduce over a communicator built once with ncclCommInitAll (xGMI
-// on MI355X nodes): SUM {sum, count} as two doubles, GROUP BY the 4097-double
-// key window of wx_group_partials.
+// on MI355X nodes): SUM {sum, count} as two doubles, GROUP BY the key window
+// plus one slot of out-of-window groups per shard (wx_group_partials_slots),
+// top-K one all-gather of wx_topk_record candidates.
 #include <hip/hip_runtime_api.h>
 #include <rccl/rccl.h>
 
@@ -180,24 +181,29 @@ Scratch &scratch_for(int device) {
   return *p;
 }
 
+// One communicator set per shard count over devices 0..n-1 (plan_shards'
+// assignment), built once and never destroyed: ResidentShards objects with
+// different shard counts each use their own set, and no set is torn down
+// while another thread may enqueue on it.  A caller holds `mu` for the whole
+// ncclGroupStart .. ncclGroupEnd of one collective.
 struct Comms {
   std::mutex mu;
   std::vector<ncclComm_t> comms;
 };
 Comms &comms_for(int ndev) {
-  static Comms c;
-  std::lock_guard<std::mutex> lk(c.mu);
-  if ((int)c.comms.size() != ndev) {
-    for (auto cm : c.comms) ncclCommDestroy(cm);
-    c.comms.assign(ndev, nullptr);
+  static std::mutex mu;
+  static auto *all = new std::map<int, std::unique_ptr<Comms>>();  // never freed (outlives HIP teardown)
+  std::lock_guard<std::mutex> lk(mu);
+  auto &p = (*all)[ndev];
+  if (!p) {
+    std::unique_ptr<Comms> c(new Comms);
+    c->comms.assign(ndev, nullptr);
     std::vector<int> devs(ndev);
     for (int i = 0; i < ndev; ++i) devs[i] = i;
-    if (ncclCommInitAll(c.comms.data(), ndev, devs.data()) != ncclSuccess) {
-      c.comms.clear();
-      throw std::runtime_error("ncclCommInitAll failed");
-    }
+    if (ncclCommInitAll(c->comms.data(), ndev, devs.data()) != ncclSuccess) throw std::runtime_error("ncclCommInitAll failed");
+    p = std::move(c);
   }
-  return c;
+  return *p;
 }
 
 }  // namespace
@@ -298,6 +304,7 @@ std::pair<double, int64_t> run_multi_gpu_sum(const HostTable &host, const std::s
 // Per-shard device buffers of the GROUP BY exchange, kept across queries.
 struct GroupScratch {
   int64_t cap = 0;
+  size_t win_doubles = 0;  // the one-collective exchange buffer (window + slots)
   DeviceBuffer win, xk, xs, xc, nx, ok, os, oc, ng;
 };
 
@@ -531,11 +538,13 @@ std::pair<double, int64_t> ResidentShards::sum(const std::string &expr_cuda, con
   return sum_over_shards(impl_->ranges, impl_->shards, expr_cuda, cond_cuda, nullptr, &impl_->sum_out);
 }
 
-// GROUP BY over the shards: per device wx_group_partials
-// (dense 2048-key window + out-of-window groups), ONE ncclAllReduce of the
-// 4097-double windows, then wx_group_combine on the first shard's device.
-// Groups outside the window (rare: keys spread wider than 2048 values) are
-// read back from every shard and merged on the host before the combine.
+// GROUP BY over the shards in ONE collective: per device
+// wx_group_partials_slots (the dense 2048-key window and this shard's slot of
+// up to 64 out-of-window groups, zeros in the others), ONE ncclAllReduce of
+// the exchange buffers (it reduces the windows and gathers the slots), then
+// wx_group_combine_slots on the first shard's device.  Only when a shard had
+// more out-of-window groups than its slot holds (WX_GROUP_NEEDS_MERGE) are
+// those groups read back from every shard and merged on the host.
 GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::string &key_cuda,
                                       const std::string &cond_cuda, int32_t key_lo) const {
   std::lock_guard<std::mutex> lk(impl_->mu);
@@ -544,15 +553,20 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
   const size_t ns = ranges.size();
   if (ns == 0) return res;
   constexpr int64_t kCap = 1 << 16;  // out-of-window groups per shard / final groups
-  constexpr size_t W = WX_GROUP_WINDOW_BINS, WD = WX_GROUP_EXCHANGE_DOUBLES;
+  constexpr int kSlotMax = 4096;     // n_slots * slot_groups bound of wx_group_combine_slots
+  const int S = std::max(1, std::min(64, kSlotMax / static_cast<int>(ns)));
+  const size_t WD = static_cast<size_t>(WX_GROUP_SLOTS_DOUBLES(ns, S));
   if (impl_->group.size() < ns) impl_->group.resize(ns);
   std::vector<double *> wins(ns, nullptr);
   std::vector<hipStream_t> streams(ns, nullptr);
   run_per_device(ranges, [&](size_t i, const ShardRange &r) {
     streams[i] = device_stream(r.device);
     GroupScratch &g = impl_->group[i];
-    if (g.cap < kCap) {
+    if (g.cap < kCap || g.win_doubles != WD) {
       g.win = DeviceBuffer(r.device, WD * 8);
+      g.win_doubles = WD;
+    }
+    if (g.cap < kCap) {
       g.xk = DeviceBuffer(r.device, kCap * 4);
       g.xs = DeviceBuffer(r.device, kCap * 8);
       g.xc = DeviceBuffer(r.device, kCap * 8);
@@ -567,10 +581,11 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
     wx_launch L = sync_launch(r.device, streams[i]);
     L.flags = 0;  // asynchronous until after the collective
     char err[8192];
-    throw_on(wx_group_partials(&v.table, val_cuda.c_str(), key_cuda.c_str(), cond_cuda.c_str(), &L, key_lo,
-                               static_cast<double *>(g.win.ptr), kCap, static_cast<int32_t *>(g.xk.ptr),
-                               static_cast<double *>(g.xs.ptr), static_cast<int64_t *>(g.xc.ptr),
-                               static_cast<int64_t *>(g.nx.ptr), nullptr, err, sizeof(err)),
+    throw_on(wx_group_partials_slots(&v.table, val_cuda.c_str(), key_cuda.c_str(), cond_cuda.c_str(), &L, key_lo,
+                                     static_cast<double *>(g.win.ptr), static_cast<int32_t>(ns),
+                                     static_cast<int32_t>(i), S, kCap, static_cast<int32_t *>(g.xk.ptr),
+                                     static_cast<double *>(g.xs.ptr), static_cast<int64_t *>(g.xc.ptr),
+                                     static_cast<int64_t *>(g.nx.ptr), nullptr, err, sizeof(err)),
              err);
     wins[i] = static_cast<double *>(g.win.ptr);
   });
@@ -580,13 +595,13 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
   char err[8192];
   wx_launch L0 = sync_launch(dev0, streams[0]);
   L0.flags = 0;
-  throw_on(wx_group_combine(static_cast<double *>(g0.win.ptr), key_lo, nullptr, nullptr, nullptr, 0, &L0, kCap,
-                            static_cast<int32_t *>(g0.ok.ptr), static_cast<double *>(g0.os.ptr),
-                            static_cast<int64_t *>(g0.oc.ptr), static_cast<int64_t *>(g0.ng.ptr), nullptr, err,
-                            sizeof(err)),
+  throw_on(wx_group_combine_slots(static_cast<double *>(g0.win.ptr), static_cast<int32_t>(ns), S, key_lo, &L0, kCap,
+                                  static_cast<int32_t *>(g0.ok.ptr), static_cast<double *>(g0.os.ptr),
+                                  static_cast<int64_t *>(g0.oc.ptr), static_cast<int64_t *>(g0.ng.ptr), nullptr, err,
+                                  sizeof(err)),
            err);
-  // the out-of-window count, the group count and the first kStage groups, in
-  // one batch of asynchronous copies behind the combine
+  // the group count and the first kStage groups, in one batch of
+  // asynchronous copies behind the combine
   constexpr int64_t kStage = 4096;
   if (!impl_->stage) {
     DevGuard dg(dev0);
@@ -595,8 +610,6 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
   char *st = impl_->stage;
   {
     DevGuard dg(dev0);
-    hip_ok(hipMemcpyAsync(st, static_cast<double *>(g0.win.ptr) + 2 * W, 8, hipMemcpyDeviceToHost, streams[0]),
-           "hipMemcpyAsync");
     hip_ok(hipMemcpyAsync(st + 8, g0.ng.ptr, 8, hipMemcpyDeviceToHost, streams[0]), "hipMemcpyAsync");
     hip_ok(hipMemcpyAsync(st + 16, g0.ok.ptr, kStage * 4, hipMemcpyDeviceToHost, streams[0]), "hipMemcpyAsync");
     hip_ok(hipMemcpyAsync(st + 16 + kStage * 4, g0.os.ptr, kStage * 8, hipMemcpyDeviceToHost, streams[0]),
@@ -604,16 +617,24 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
     hip_ok(hipMemcpyAsync(st + 16 + kStage * 12, g0.oc.ptr, kStage * 8, hipMemcpyDeviceToHost, streams[0]),
            "hipMemcpyAsync");
   }
-  for (size_t i = 0; i < ns; ++i) {  // every shard's device errors (and the collective) complete
+  // every shard's stream (and the collective) complete; the decisions below
+  // come from the combined buffer only, so a shard's own capacity flag is
+  // reported through it (the same error whichever shard hit it)
+  std::exception_ptr shard_err;
+  for (size_t i = 0; i < ns; ++i) {
     DevGuard dg(ranges[i].device);
     hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
     wx_launch L = sync_launch(ranges[i].device, streams[i]);
-    throw_on(wx_check(&L, err, sizeof(err)), err);
+    if (wx_check(&L, err, sizeof(err)) != WX_OK && !shard_err)
+      shard_err = std::make_exception_ptr(std::runtime_error(err));
   }
-  double n_extra_total = 0;
-  std::memcpy(&n_extra_total, st, 8);
+  int64_t ng = 0;
+  std::memcpy(&ng, st + 8, 8);
+  if (ng == -1) throw std::runtime_error("group table / output capacity exceeded (general-key table overflow)");
+  if (shard_err) std::rethrow_exception(shard_err);
+  const bool merged_extra = ng == WX_GROUP_NEEDS_MERGE;
   DeviceBuffer mk, ms, mc;
-  if (n_extra_total > 0) {
+  if (merged_extra) {
     std::map<int32_t, std::pair<double, int64_t>> merged;
     for (size_t i = 0; i < ns; ++i) {
       GroupScratch &g = impl_->group[i];
@@ -657,19 +678,14 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
                               static_cast<int64_t *>(g0.oc.ptr), static_cast<int64_t *>(g0.ng.ptr), nullptr, err,
                               sizeof(err)),
              err);
+    hip_ok(hipMemcpy(&ng, g0.ng.ptr, 8, hipMemcpyDeviceToHost), "hipMemcpy");  // combined again: the new count
   }
   DevGuard dg(dev0);
-  int64_t ng = 0;
-  if (n_extra_total > 0) {  // combined again with the out-of-window groups: read the new result
-    hip_ok(hipMemcpy(&ng, g0.ng.ptr, 8, hipMemcpyDeviceToHost), "hipMemcpy");
-  } else {
-    std::memcpy(&ng, st + 8, 8);
-  }
   if (ng > kCap) throw std::runtime_error("group table / output capacity exceeded");
   res.keys.resize(ng);
   res.sums.resize(ng);
   res.counts.resize(ng);
-  if (ng && n_extra_total == 0 && ng <= kStage) {  // the staged copies hold the whole result
+  if (ng && !merged_extra && ng <= kStage) {  // the staged copies hold the whole result
     std::memcpy(res.keys.data(), st + 16, ng * 4);
     std::memcpy(res.sums.data(), st + 16 + kStage * 4, ng * 8);
     std::memcpy(res.counts.data(), st + 16 + kStage * 12, ng * 8);

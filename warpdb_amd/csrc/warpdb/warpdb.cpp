@@ -204,14 +204,16 @@ void WarpDB::query_arrow_device(const std::string &expr, ArrowDeviceArray *out_a
 // GPU holding table_ the shard IS table_ (borrowed, no second HBM copy).
 warpdb::ResidentShards &WarpDB::shards() {
   if (host_table_.num_rows() == 0) throw std::runtime_error("Host table not available for multi-GPU query");
-  if (!shards_) {
+  // call_once: two threads' first multi-GPU calls (GIL released) build one set
+  // of shards; a throwing build leaves the flag unset, so the next call retries
+  std::call_once(shards_once_, [this] {
     int ndev = 0;
     hip_ok(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
     if (ndev == 1 && table_.device == 0 && !std::getenv("WARPDB_VIRTUAL_SHARDS"))  // (test hook: multi_gpu.cpp)
       shards_ = warpdb::ResidentShards::borrow(table_);
     else
       shards_ = std::make_unique<warpdb::ResidentShards>(host_table_);
-  }
+  });
   return *shards_;
 }
 
@@ -265,6 +267,9 @@ warpdb::GroupResult WarpDB::query_multi_gpu_group(const std::string &sql, int32_
   if (!ast.group_by || !agg) throw std::runtime_error("query_multi_gpu_group expects SELECT <agg>(expr) ... GROUP BY key");
   if (ast.group_by->keys.size() != 1) throw std::runtime_error("GROUP BY supports one key expression");
   if (!ast.joins.empty()) throw std::runtime_error("JOIN is not supported by the execution engine");
+  const std::string kind = agg->agg_kernel();
+  if (kind != "sum" && kind != "count" && kind != "avg")  // the shards exchange (sum, count) only
+    throw std::runtime_error("query_multi_gpu_group supports SUM / COUNT / AVG, not " + kind);
   validate_ast(agg->expr.get(), cols);
   validate_ast(ast.group_by->keys[0].get(), cols);
   std::string cond;

@@ -11,13 +11,17 @@ the C ABI.  The exchanges are the ones the result needs, one collective each
                order)
   SUM          all-reduce of {sum, count} as two doubles (the count is exact
                below 2^53; WX_F_F64_COUNTS writes it that way)
-  GROUP BY     all-reduce of the dense key window (2048 sums, 2048 counts,
-               1 out-of-window group count: 4097 doubles); only when some
-               shard saw keys outside the window, an all-gather merge of
-               those groups follows
-  top-K        all-gather of K packed candidates (key, value, row) + count
-               per shard, merged by (key, row) -- on the host (merge_topk) or,
-               without a host round trip, on the device (merge_topk_device)
+  GROUP BY     ONE all-reduce of the exchange buffer: the dense key window
+               (2048 sums, 2048 counts, 1 out-of-window group count) and one
+               slot per shard holding its first 64 out-of-window groups, zero
+               elsewhere, so the same SUM both reduces the window and gathers
+               the slots; wx_group_combine_slots merges them on the device.
+               Only when a shard had more out-of-window groups than its slot
+               holds (every rank sees it in the same combined buffer) does a
+               variable-size all-gather merge follow
+  top-K        all-gather of one 520-byte wx_topk_record per shard (K keys,
+               values, global rows, count), merged by wx_topk_merge on the
+               device (better key, NaN last, then the smaller row)
 
 With the "nccl" backend these run on RCCL over xGMI on device tensors; with
 "gloo" (CPU tests, or several ranks sharing one GPU) the same code stages
@@ -127,6 +131,35 @@ def exchange_group_window(window: torch.Tensor, group=None) -> torch.Tensor:
     return all_reduce_(window, group=group)
 
 
+GROUP_SLOT_MAX = 4096  # n_slots * slot_groups bound of wx_group_combine_slots
+
+
+def group_slot_groups(world: int) -> int:
+    """Out-of-window groups each shard's exchange slot carries (64, fewer
+    above 64 ranks so that world * slot_groups stays <= 4096)."""
+    return max(1, min(64, GROUP_SLOT_MAX // max(1, world)))
+
+
+def group_slot_counts(exchange: torch.Tensor, world: int, slot_groups: int) -> List[int]:
+    """Every shard's out-of-window group count from a combined exchange buffer
+    (-1: that shard's general-key table overflowed)."""
+    sl = 1 + 3 * slot_groups
+    slots = exchange.reshape(-1)[GROUP_EXCHANGE_DOUBLES:GROUP_EXCHANGE_DOUBLES + world * sl]
+    return [int(x) for x in slots.view(world, sl)[:, 0].tolist()]
+
+
+def group_exchange_error(counts: List[int], capacity: int) -> Optional[str]:
+    """The error every rank raises after the exchange, or None.  It depends
+    only on the combined buffer, which is the same on every rank, so no rank
+    raises alone while the others wait in the next collective."""
+    for r, c in enumerate(counts):
+        if c < 0:
+            return f"shard {r}: general-key group table overflowed"
+        if c > capacity:
+            return f"shard {r}: {c} groups outside the key window exceed capacity {capacity}"
+    return None
+
+
 def _gather_padded(t: torch.Tensor, n: int, group=None) -> Tuple[torch.Tensor, List[int]]:
     """All-gather the first n entries of t from every rank (variable n)."""
     world = _world(group)
@@ -155,80 +188,39 @@ def merge_groups(keys: torch.Tensor, sums: torch.Tensor, counts: torch.Tensor, n
 
 
 # ------------------------------------------------------------------ top-K
-def _f32_bits(x: torch.Tensor) -> torch.Tensor:
-    return x.to(torch.float32).contiguous().view(torch.int32).to(torch.int64) & 0xFFFFFFFF
+TOPK_MAX = 32
+TOPK_RECORD_BYTES = TOPK_MAX * 16 + 8  # wx_topk_record (include/warpexec.h)
 
 
-def exchange_topk(keys: torch.Tensor, idx: torch.Tensor, vals: torch.Tensor, n: int, k: int, group=None):
-    """All shards' candidates from one all-gather: per shard an int64[2k + 1]
-    record (count, then k x (key bits << 32 | value bits, row))."""
-    dev = keys.device if not _host_staged(group) else torch.device("cpu")
-    rec = torch.zeros(2 * k + 1, dtype=torch.int64, device=dev)
-    rec[0] = n
-    if n:
-        kv = (_f32_bits(keys[:n]) << 32) | _f32_bits(vals[:n])
-        rec[1: 1 + 2 * n: 2] = kv.to(dev)
-        rec[2: 2 + 2 * n: 2] = idx[:n].to(torch.int64).to(dev)
-    allr = all_gather(rec, group).cpu().view(-1, 2 * k + 1)
-    ks, vs, rs = [], [], []
-    for r in range(allr.shape[0]):
-        m = int(allr[r, 0])
-        body = allr[r, 1: 1 + 2 * m].view(-1, 2)
-        kv = body[:, 0]
-        ks.append(((kv >> 32) & 0xFFFFFFFF).to(torch.int32).view(torch.float32))
-        vs.append((kv & 0xFFFFFFFF).to(torch.int32).view(torch.float32))
-        rs.append(body[:, 1])
-    return torch.cat(ks), torch.cat(rs), torch.cat(vs)
+def topk_record_views(rec: torch.Tensor):
+    """(keys f32[32], vals f32[32], rows i64[32], count i64[1]) views of one
+    wx_topk_record held in a uint8 tensor of TOPK_RECORD_BYTES."""
+    if rec.dtype != torch.uint8 or rec.numel() != TOPK_RECORD_BYTES:
+        raise ValueError("a top-K record is uint8[520]")
+    return (rec[0:128].view(torch.float32), rec[128:256].view(torch.float32), rec[256:512].view(torch.int64),
+            rec[512:520].view(torch.int64))
 
 
-def merge_topk_candidates(gk: torch.Tensor, gi: torch.Tensor, gv: torch.Tensor, k: int, descending: bool):
-    """Global top-K of gathered candidates; ties by ascending row index, NaN last."""
-    order = torch.argsort(gi, stable=True)
-    gk, gi, gv = gk[order], gi[order], gv[order]
-    key = torch.where(torch.isnan(gk), torch.full_like(gk, float("inf") if not descending else -float("inf")), gk)
-    order = torch.argsort(key, descending=descending, stable=True)
-    nan_last = torch.isnan(gk[order])
-    order = torch.cat([order[~nan_last], order[nan_last]])[:k]
-    return gk[order], gi[order], gv[order]
+def exchange_topk_records(rec: torch.Tensor, group=None) -> torch.Tensor:
+    """Every shard's candidate record, concatenated in rank order: ONE
+    all-gather of 520 bytes per shard (RCCL on device tensors)."""
+    return all_gather(rec, group)
 
 
-def merge_topk(keys: torch.Tensor, idx: torch.Tensor, vals: torch.Tensor, n: int, k: int, descending: bool,
-               group=None):
-    """Global top-K from per-shard candidates (one all-gather, then the merge)."""
-    gk, gi, gv = exchange_topk(keys, idx, vals, n, k, group)
-    return merge_topk_candidates(gk, gi, gv, k, descending)
+def merge_topk_device(rec: torch.Tensor, k: int, descending: bool, launch, out_k: torch.Tensor,
+                      out_i: torch.Tensor, out_v: torch.Tensor, out_n: torch.Tensor, group=None):
+    """Global top-K left in HBM with no host round trip: the all-gather of the
+    shards' records, then wx_topk_merge (one HIP kernel: better key first, NaN
+    last, ties by the smaller row).  Returns (keys, rows, vals, count)."""
+    from . import _warpexec as wx
 
-
-def merge_topk_device(keys: torch.Tensor, idx: torch.Tensor, vals: torch.Tensor, count: torch.Tensor, k: int,
-                      descending: bool, group=None):
-    """merge_topk without a host round trip: one all-gather of every shard's
-    k candidate slots (unused slots masked by the shard's device-side count),
-    then stable sorts on the device -- by row, by key, by class (number,
-    NaN, unused slot) -- so ties keep the smallest row and NaN sorts last.
-    Returns (keys, rows, vals) of k slots and the global count min(k, total),
-    all on the device of `keys` (gloo stages through the host)."""
-    dev = keys.device
-    if _single(group):  # one shard's list is final (its count is already <= k)
-        return keys[:k], idx[:k], vals[:k], count.reshape(1)
-    rec = torch.zeros(2 * k + 1, dtype=torch.int64, device=dev)
-    rec[0:1] = count.reshape(1).to(torch.int64)
-    rec[1: 1 + 2 * k: 2] = (_f32_bits(keys[:k]) << 32) | _f32_bits(vals[:k])
-    rec[2: 2 + 2 * k: 2] = idx[:k].to(torch.int64)
-    allr = all_gather(rec, group).view(-1, 2 * k + 1)
-    n = allr[:, 0:1]
-    body = allr[:, 1:].reshape(-1, k, 2)
-    kv, gi = body[:, :, 0].reshape(-1), body[:, :, 1].reshape(-1)
-    gk = ((kv >> 32) & 0xFFFFFFFF).to(torch.int32).view(torch.float32)
-    gv = (kv & 0xFFFFFFFF).to(torch.int32).view(torch.float32)
-    used = (torch.arange(k, device=dev).reshape(1, k) < n).reshape(-1)
-    cls = torch.where(used, torch.isnan(gk).to(torch.int64), torch.full_like(gi, 2))
-    fill = float("-inf") if descending else float("inf")
-    key = torch.where(cls == 0, gk, torch.full_like(gk, fill))
-    order = torch.argsort(gi, stable=True)
-    order = order[torch.argsort(key[order], descending=descending, stable=True)]
-    order = order[torch.argsort(cls[order], stable=True)][:k]
-    total = torch.clamp(n.sum().reshape(1), max=k)
-    return gk[order], gi[order], gv[order], total
+    if rec.device.type != "cuda":
+        raise RuntimeError("merge_topk_device runs on the GPU (wx_topk_merge); no CPU path exists")
+    allr = exchange_topk_records(rec, group)
+    n_rec = allr.numel() // TOPK_RECORD_BYTES
+    wx.topk_merge(allr.data_ptr(), n_rec, k, descending, launch, out_k.data_ptr(), out_i.data_ptr(),
+                  out_v.data_ptr(), out_n.data_ptr())
+    return out_k[:k], out_i[:k], out_v[:k], out_n
 
 
 @dataclass
@@ -312,80 +304,101 @@ class ShardedQuery:
         return float(h[0]), int(h[1])
 
     # --- GROUP BY ---------------------------------------------------------
+    def _group_bufs(self, capacity: int):
+        wx = self.wx
+        S = group_slot_groups(self.world)
+        nd = wx.group_slots_doubles(self.world, S)
+        return (S, self._buf("gex", nd, torch.float64)[:nd], self._buf("gxk", capacity, torch.int32),
+                self._buf("gxs", capacity, torch.float64), self._buf("gxc", capacity, torch.int64),
+                self._buf("gnx", 1, torch.int64), self._buf("gok", capacity, torch.int32),
+                self._buf("gos", capacity, torch.float64), self._buf("goc", capacity, torch.int64),
+                self._buf("gng", 1, torch.int64))
+
     def group_sum_device(self, val_expr: str, key_expr: str, cond: Optional[str], key_lo: int = 0,
                          capacity: int = 1 << 16):
-        """GROUP BY over every shard: per-shard partials, ONE all-reduce of
-        the 4097-double window, the final merge on the device.  Returns
-        (keys, sums, counts, n_groups) device tensors of `capacity` entries;
-        reads one double back to learn whether any shard saw keys outside
-        the window (then their groups are all-gathered and merged).  With a
-        single shard it is wx_group_sum alone (asynchronous)."""
+        """GROUP BY over every shard with no host synchronisation: per-shard
+        partials written straight into the one-collective exchange layout
+        (window + this shard's slot of out-of-window groups), ONE all-reduce,
+        the final merge on the device (wx_group_combine_slots).  Returns
+        (keys, sums, counts, n_groups) device tensors of `capacity` entries.
+        n_groups reads GROUP_NEEDS_MERGE (-2) when some shard had more
+        out-of-window groups than its slot holds -- the same value on every
+        rank -- and group_sum then takes the variable-size merge; -1 when a
+        shard's general-key table overflowed.  One shard: wx_group_sum alone."""
         wx = self.wx
-        window = self._buf("gwin", GROUP_EXCHANGE_DOUBLES, torch.float64)[:GROUP_EXCHANGE_DOUBLES]
-        xk = self._buf("gxk", capacity, torch.int32)
-        xs = self._buf("gxs", capacity, torch.float64)
-        xc = self._buf("gxc", capacity, torch.int64)
-        nx = self._buf("gnx", 1, torch.int64)
-        ok = self._buf("gok", capacity, torch.int32)
-        osm = self._buf("gos", capacity, torch.float64)
-        oc = self._buf("goc", capacity, torch.int64)
-        ng = self._buf("gng", 1, torch.int64)
+        S, ex, xk, xs, xc, nx, ok, osm, oc, ng = self._group_bufs(capacity)
         if self.world == 1:  # one shard: the single-GPU kernel + finalize, nothing to exchange or read back
             wx.group_sum(self.table, val_expr, key_expr, cond, self.launch, key_lo, capacity, ok.data_ptr(),
                          osm.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr(), want_count=False)
             return ok, osm, oc, ng
-        wx.group_partials(self.table, val_expr, key_expr, cond, self.launch, key_lo, window.data_ptr(), capacity,
-                          xk.data_ptr(), xs.data_ptr(), xc.data_ptr(), d_n_extra=nx.data_ptr())
-        exchange_group_window(window, self.group)
-        wx.group_combine(window.data_ptr(), key_lo, 0, 0, 0, 0, self.launch_aux, capacity, ok.data_ptr(),
-                         osm.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr())
-        if window[2 * GROUP_WINDOW_BINS].item() != 0.0:  # keys outside the window on some shard
-            mk, ms, mc = merge_groups(xk, xs, xc, int(nx.item()), self.group)
-            mk, ms, mc = mk.cuda(), ms.cuda(), mc.cuda()
-            wx.group_combine(window.data_ptr(), key_lo, mk.data_ptr(), ms.data_ptr(), mc.data_ptr(), mk.numel(),
-                             self.launch_aux, capacity, ok.data_ptr(), osm.data_ptr(), oc.data_ptr(),
-                             d_n_groups=ng.data_ptr())
-            self._keep = (mk, ms, mc)  # alive until the stream has consumed them
+        wx.group_partials_slots(self.table, val_expr, key_expr, cond, self.launch, key_lo, ex.data_ptr(), self.world,
+                                _rank(self.group), S, capacity, xk.data_ptr(), xs.data_ptr(), xc.data_ptr(),
+                                d_n_extra=nx.data_ptr())
+        all_reduce_(ex, group=self.group)
+        wx.group_combine_slots(ex.data_ptr(), self.world, S, key_lo, self.launch_aux, capacity, ok.data_ptr(),
+                               osm.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr())
         return ok, osm, oc, ng
 
     def group_sum(self, val_expr: str, key_expr: str, cond: Optional[str], key_lo: int = 0,
                   capacity: int = 1 << 16):
+        """GROUP BY over every shard as device tensors of the final groups.
+        Every decision after the exchange is taken from the all-reduced
+        buffer, which is identical on every rank, so the ranks raise or take
+        the fallback merge together (never one rank alone)."""
+        wx = self.wx
         ok, osm, oc, ng = self.group_sum_device(val_expr, key_expr, cond, key_lo, capacity)
+        n = int(ng.item())  # synchronises
+        if self.world > 1:
+            S, ex, xk, xs, xc, nx = self._group_bufs(capacity)[:6]
+            counts = group_slot_counts(ex.cpu(), self.world, S)
+            err = group_exchange_error(counts, capacity)
+            if err is not None:
+                try:
+                    wx.check(self.launch)  # clear this shard's own flag (the same condition)
+                except wx.WarpExecError:
+                    pass
+                raise wx.WarpExecError(wx.WX_ERR_CAPACITY, err)
+            if n == wx.GROUP_NEEDS_MERGE:  # some shard's out-of-window groups outgrew its slot
+                m = int(counts[_rank(self.group)])
+                mk, ms, mc = merge_groups(xk, xs, xc, m, self.group)
+                mk, ms, mc = mk.cuda(), ms.cuda(), mc.cuda()
+                # identical merged groups on every rank: a capacity error is raised by all of them
+                n = wx.group_combine(ex.data_ptr(), key_lo, mk.data_ptr(), ms.data_ptr(), mc.data_ptr(), mk.numel(),
+                                     self.launch_aux, capacity, ok.data_ptr(), osm.data_ptr(), oc.data_ptr(),
+                                     d_n_groups=ng.data_ptr(), want_count=True)
         self.wx.check(self.launch)
-        n = int(ng.item())
-        if n > capacity:
+        if n > capacity or n < 0:
             raise self.wx.WarpExecError(self.wx.WX_ERR_CAPACITY, f"{n} groups exceed capacity {capacity}")
         return ok[:n].clone(), osm[:n].clone(), oc[:n].clone()
 
     # --- top-K ------------------------------------------------------------
     def topk_device(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int,
                     descending: bool):
-        """This shard's top-K (keys, global rows, SELECT values, count) on the
-        device, asynchronous; ties by ascending row index, NaN last."""
-        tk = self._buf("tk", k, torch.float32)
-        ti = self._buf("ti", k, torch.int64)
-        tv = self._buf("tv", k, torch.float32)
-        tn = self._buf("tn", 1, torch.int64)
-        self.wx.topk(self.table, order_expr, cond, select_expr, k, descending, self.launch, tk.data_ptr(),
-                     ti.data_ptr(), tv.data_ptr(), row_base=self.shard.row_base, d_count=tn.data_ptr(),
+        """This shard's top-K written straight into its wx_topk_record
+        (keys, global rows, SELECT values, count), asynchronous; ties by
+        ascending row index, NaN last.  Returns the record (uint8[520])."""
+        rec = self._buf("trec", TOPK_RECORD_BYTES, torch.uint8)[:TOPK_RECORD_BYTES]
+        rk, rv, ri, rn = topk_record_views(rec)
+        self.wx.topk(self.table, order_expr, cond, select_expr, k, descending, self.launch, rk.data_ptr(),
+                     ri.data_ptr(), rv.data_ptr(), row_base=self.shard.row_base, d_count=rn.data_ptr(),
                      want_count=False)
-        return tk, ti, tv, tn
+        return rec
 
     def topk_merged_device(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int,
                            descending: bool):
         """Global top-K left in HBM, no host synchronisation: this shard's
-        candidates, then merge_topk_device.  Returns (keys, rows, vals, count)."""
-        tk, ti, tv, tn = self.topk_device(order_expr, cond, select_expr, k, descending)
-        return merge_topk_device(tk, ti, tv, tn, k, descending, self.group)
+        record, one all-gather, wx_topk_merge.  Returns (keys, rows, vals, count)."""
+        rec = self.topk_device(order_expr, cond, select_expr, k, descending)
+        if self.world == 1:  # one shard's list is final (its count is already <= k)
+            rk, rv, ri, rn = topk_record_views(rec)
+            return rk[:k], ri[:k], rv[:k], rn
+        return merge_topk_device(rec, k, descending, self.launch_aux, self._buf("tmk", k, torch.float32),
+                                 self._buf("tmi", k, torch.int64), self._buf("tmv", k, torch.float32),
+                                 self._buf("tmn", 1, torch.int64), self.group)
 
     def topk(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int, descending: bool):
-        """Global top-K as host tensors: one all-gather of every shard's K
-        candidates, then the (key, row) merge; a single shard is already final."""
-        tk, ti, tv, tn = self.topk_device(order_expr, cond, select_expr, k, descending)
-        if self.world == 1:
-            m = int(tn.item())  # synchronises
-            self.wx.check(self.launch)
-            return tk[:m].cpu(), ti[:m].cpu(), tv[:m].cpu()
-        m = int(tn.item())
+        """Global top-K as host tensors (topk_merged_device + one read-back)."""
+        tk, ti, tv, tn = self.topk_merged_device(order_expr, cond, select_expr, k, descending)
+        m = int(tn.reshape(-1)[0].item())  # synchronises
         self.wx.check(self.launch)
-        return merge_topk(tk, ti, tv, m, k, descending, self.group)
+        return tk[:m].cpu(), ti[:m].cpu(), tv[:m].cpu()
