@@ -503,6 +503,13 @@ def main_ranks(args):
         bytes_per_launch = n * 8 + passing * 8  # 4 B value + 4 B int32 index per passing row
     elif workload == "dense":
         bytes_per_launch = n * 12
+    elif workload == "group" and launches > args.steps:
+        # many keys: the range-partitioned pipeline (probe, hist, scan, scatter,
+        # LDS aggregation, emit) as one unit per step; algorithmic bytes are
+        # still the 8 B/row the query reads (the roofline BASELINE prices)
+        kern_avg_ms *= launches / max(1, args.steps)
+        kname = "wx_group_part_* pipeline (probe + hist + scatter + agg + emit)"
+        bytes_per_launch = n * rb
     elif workload == "sort":  # histogram read + the tile passes that ran (read + write 4 B each)
         passes = max(0, round(launches / max(1, args.steps)) - 1)
         kern_avg_ms *= launches / max(1, args.steps)  # the sort's kernels as one unit: per step
@@ -529,6 +536,8 @@ def main_ranks(args):
                                             "copy, as WarpDB::query_sql)" if src is not None
                                             else "the compacted projection")
         line["check"] = check
+        if workload == "group":
+            line["config"]["distinct_keys"] = args.keys
         line["roofline"] = roofline(bytes_per_launch, kern_avg_ms, n * rb, kname, pmc_traffic(workload, n),
                                     "HIP events around the dominant kernel on its stream (max over ranks)")
     # The other north-star aggregates on the same shards, timed the same way

@@ -17,6 +17,7 @@ typedef unsigned int wx_u32;
 #define WX_DEVERR_LOOKBACK 1u
 #define WX_DEVERR_CAPACITY 2u
 #define WX_DEVERR_UNSUPPORTED 4u
+#define WX_DEVERR_INTERNAL_KEY 8u  // a partitioned GROUP BY key fell outside its probed range (internal)
 
 #define WX_OP_DENSE 0
 #define WX_OP_COMPACT 1
@@ -149,6 +150,40 @@ struct WxGroupSlotsArgs {
   wx_i64 *out_counts;
   wx_i64 capacity;
   wx_i64 *n_groups_out;  // -1: a shard's general-key table overflowed; -2: a slot overflowed (merge needed)
+};
+
+// Range-partitioned GROUP BY for many distinct keys (wx_group_part_*): the
+// passing rows' keys span [key_lo, key_lo + span); partition p holds keys
+// [key_lo + p << shift, key_lo + (p + 1) << shift).  Rows are scattered as
+// (bin << 32 | value bits) pairs into partition-contiguous order, each
+// partition is aggregated in an LDS window of 1 << shift bins, and the dense
+// per-key results are compacted in ascending key order.
+#define WX_GP_BLOCK 1024
+struct WxGroupPartArgs {
+  const void *col[WX_MAX_COLS];
+  wx_i64 n_rows;
+  wx_i64 rows_per_wg;  // hist / scatter: contiguous rows per workgroup (a multiple of 4)
+  int n_wg;            // G: hist / scatter workgroups
+  int n_part;          // P
+  int key_lo;
+  int shift;
+  wx_i64 *mm;           // [gridDim.x][3] per-workgroup (min key, max key, passing rows) of the probe
+  wx_u32 *pcount;       // [P][G] rows of partition p in workgroup g's range
+  wx_i64 *poff;         // [P][G] first pair slot of (p, g)
+  wx_u64 *pairs;        // [passing rows] (bin << 32 | value bits), partition-contiguous
+  wx_i64 *work;         // [n_work][2]: (p << 40 | whole-partition flag << 39 | len, start)
+  wx_i64 *n_work;
+  wx_i64 work_cap;
+  wx_i64 chunk;         // pairs per aggregation work item
+  double *dsum;         // [P << shift] dense per-key sums (zero between calls)
+  wx_u64 *dcnt;         // [P << shift] dense per-key counts (zero between calls)
+  wx_u32 *pnz;          // [P] non-empty keys per partition
+  int *out_keys;
+  double *out_sums;
+  wx_i64 *out_counts;
+  wx_i64 capacity;
+  wx_i64 *n_groups_out;
+  wx_u64 *ctrs;  // [1]: error bits
 };
 
 // Top-K exchange record of one shard (wx_topk_record in warpexec.h)

@@ -1425,6 +1425,342 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs 
   }
 }
 
+// ---------------------------------------------------------------------------
+// Range-partitioned GROUP BY (many distinct keys).  With 1e6 keys and 1e9
+// rows every workgroup sees each key about once, so neither the LDS window nor
+// a per-workgroup LDS hash can absorb anything and the global hash pays two
+// memory-side atomics per row (9.1 ms per 1e8 rows, 1 % of the read
+// roofline).  Instead the rows are partitioned by key range so that each
+// partition fits an LDS window:
+//   probe    exact (min, max) key and passing rows, per workgroup (host reduces)
+//   hist     per workgroup (static contiguous row ranges): rows per partition
+//   scan     one workgroup: partition-major offsets + aggregation work items
+//   scatter  same row ranges: (bin, value) pairs to partition-contiguous slots
+//   agg      per work item (a chunk of one partition): LDS window of 1 << shift
+//            bins (ds_add_f64 / ds_add_u32), flushed to dense per-key arrays
+//   count / scan2 / emit   non-empty keys per partition, their prefix, and the
+//            outputs in ascending key order; the dense arrays are re-zeroed
+#define WX_GP_UNROLL 2
+#define WX_GP_SPAN ((wx_i64)WX_GP_BLOCK * WX_GP_UNROLL)
+#define WX_GP_QUAD(u) (wx_base + (wx_i64)(u) * WX_GP_BLOCK + threadIdx.x)
+#define WX_DECL_GP(name, T, slot) T wx_u##slot[WX_GP_UNROLL][4];
+#define WX_LOAD_GP_FAST(name, T, slot) ::wx::load4_full<T>(wx_a.col[slot], wx_r0u, wx_u##slot[wx_u]);
+#define WX_LOAD_GP(name, T, slot) ::wx::load4_tail<T>(wx_a.col[slot], wx_r0u, wx_rend, wx_u##slot[wx_u]);
+// rows [RB, RE) of this workgroup (RB a multiple of 4), WX_GP_SPAN quads per step
+#define WX_RANGE_LOOP_BEGIN(RB, RE)                                                                 \
+  const wx_i64 wx_rend = (RE);                                                                      \
+  const wx_i64 wx_qe = (wx_rend + 3) >> 2, wx_qfull = wx_rend >> 2;                                 \
+  for (wx_i64 wx_base = (RB) >> 2; wx_base < wx_qe; wx_base += WX_GP_SPAN) {                        \
+    WX_COLS(WX_DECL_GP)                                                                             \
+    if (WX_ALIGNED16 && wx_base + WX_GP_SPAN <= wx_qfull) {                                         \
+      _Pragma("unroll") for (int wx_u = 0; wx_u < WX_GP_UNROLL; ++wx_u) {                          \
+        const wx_i64 wx_r0u = WX_GP_QUAD(wx_u) << 2;                                                \
+        WX_COLS(WX_LOAD_GP_FAST)                                                                    \
+      }                                                                                             \
+    } else {                                                                                        \
+      _Pragma("unroll") for (int wx_u = 0; wx_u < WX_GP_UNROLL; ++wx_u) {                          \
+        const wx_i64 wx_r0u = WX_GP_QUAD(wx_u) << 2;                                                \
+        WX_COLS(WX_LOAD_GP)                                                                         \
+      }                                                                                             \
+    }                                                                                               \
+    _Pragma("unroll") for (int wx_u = 0; wx_u < WX_GP_UNROLL; ++wx_u) {                            \
+      const wx_i64 wx_r0 = WX_GP_QUAD(wx_u) << 2;                                                   \
+      if (WX_GP_QUAD(wx_u) < wx_qe) {                                                               \
+        _Pragma("unroll") for (int wx_e = 0; wx_e < 4; ++wx_e) {                                   \
+          WX_COLS(WX_BIND_U)                                                                        \
+          const wx_i64 idx = wx_r0 + wx_e;
+#define WX_RANGE_LOOP_END \
+  }                       \
+  }                       \
+  }                       \
+  }
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_part_minmax(WxGroupPartArgs wx_a) {
+  __shared__ int s_mn[WX_WAVES], s_mx[WX_WAVES];
+  __shared__ wx_u64 s_c[WX_WAVES];
+  int wx_mn = 0x7fffffff, wx_mx = (int)0x80000000;
+  wx_u64 wx_c = 0;
+  WX_STRIDE_LOOP_BEGIN
+  if (idx < wx_a.n_rows && WX_EVAL_COND()) {
+    const int wx_k = static_cast<int>(WX_KEY);
+    wx_mn = wx_k < wx_mn ? wx_k : wx_mn;
+    wx_mx = wx_k > wx_mx ? wx_k : wx_mx;
+    ++wx_c;
+  }
+  WX_STRIDE_LOOP_END
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int a = __shfl_xor(wx_mn, o), b = __shfl_xor(wx_mx, o);
+    wx_mn = a < wx_mn ? a : wx_mn;
+    wx_mx = b > wx_mx ? b : wx_mx;
+    wx_c += __shfl_xor(wx_c, o);
+  }
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  if (lane == 0) { s_mn[wave] = wx_mn; s_mx[wave] = wx_mx; s_c[wave] = wx_c; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < WX_WAVES; ++w) {
+      wx_mn = s_mn[w] < wx_mn ? s_mn[w] : wx_mn;
+      wx_mx = s_mx[w] > wx_mx ? s_mx[w] : wx_mx;
+      wx_c += s_c[w];
+    }
+    wx_a.mm[3 * blockIdx.x] = wx_mn;
+    wx_a.mm[3 * blockIdx.x + 1] = wx_mx;
+    wx_a.mm[3 * blockIdx.x + 2] = (wx_i64)wx_c;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_hist(WxGroupPartArgs wx_a) {
+  extern __shared__ wx_u32 wx_s_dyn[];
+  wx_u32 *s_h = wx_s_dyn;  // [P]
+  for (int i = threadIdx.x; i < wx_a.n_part; i += WX_GP_BLOCK) s_h[i] = 0u;
+  __syncthreads();
+  const wx_i64 wx_rb = (wx_i64)blockIdx.x * wx_a.rows_per_wg;
+  const wx_i64 wx_re = wx_rb + wx_a.rows_per_wg < wx_a.n_rows ? wx_rb + wx_a.rows_per_wg : wx_a.n_rows;
+  {
+    WX_RANGE_LOOP_BEGIN(wx_rb, wx_re)
+    if (idx < wx_rend && WX_EVAL_COND()) {
+      const wx_u32 wx_p = ((wx_u32) static_cast<int>(WX_KEY) - (wx_u32)wx_a.key_lo) >> wx_a.shift;
+      if (wx_p < (wx_u32)wx_a.n_part) atomicAdd(&s_h[wx_p], 1u);
+      else atomicOr(reinterpret_cast<unsigned int *>(&wx_a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+    }
+    WX_RANGE_LOOP_END
+  }
+  __syncthreads();
+  for (int p = threadIdx.x; p < wx_a.n_part; p += WX_GP_BLOCK)
+    wx_a.pcount[(wx_i64)p * wx_a.n_wg + blockIdx.x] = s_h[p];
+}
+
+// Exclusive scan of a device array of n values (one 1024-thread block, 4
+// consecutive values per thread per step); returns the total to every thread.
+template <typename In, typename Out>
+__device__ __forceinline__ wx_i64 wx_block_scan_excl(const In *in, Out *out, wx_i64 n, wx_i64 *s_w) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  wx_i64 carry = 0;
+  for (wx_i64 base = 0; base < n; base += 4 * 1024) {
+    wx_i64 v[4], loc = 0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const wx_i64 i = base + (wx_i64)tid * 4 + j;
+      v[j] = i < n ? (wx_i64)in[i] : 0;
+      loc += v[j];
+    }
+    wx_i64 incl = loc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_i64 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    wx_i64 wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const wx_i64 x = s_w[w];
+      wb += w < wave ? x : 0;
+      tot += x;
+    }
+    wx_i64 run = carry + wb + incl - loc;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const wx_i64 i = base + (wx_i64)tid * 4 + j;
+      if (i < n) out[i] = (Out)run;
+      run += v[j];
+    }
+    carry += tot;
+    __syncthreads();
+  }
+  return carry;
+}
+
+extern "C" __global__ __launch_bounds__(1024) void wx_group_part_scan(WxGroupPartArgs a) {
+  __shared__ wx_i64 s_w[16];
+  __shared__ wx_i64 s_items;
+  const wx_i64 total = wx_block_scan_excl(a.pcount, a.poff, (wx_i64)a.n_part * a.n_wg, s_w);
+  __syncthreads();
+  // work items: each partition in chunks of a.chunk pairs; prefix of the
+  // per-partition chunk counts by a scan over P (<= 8 per thread)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_items = 0;
+  __syncthreads();
+  for (int p0 = 0; p0 < a.n_part; p0 += 1024) {
+    const int p = p0 + tid;
+    wx_i64 st = 0, len = 0, nch = 0;
+    if (p < a.n_part) {
+      st = a.poff[(wx_i64)p * a.n_wg];
+      const wx_i64 en = p + 1 < a.n_part ? a.poff[(wx_i64)(p + 1) * a.n_wg] : total;
+      len = en - st;
+      nch = (len + a.chunk - 1) / a.chunk;
+    }
+    wx_i64 incl = nch;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_i64 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    wx_i64 wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const wx_i64 x = s_w[w];
+      wb += w < wave ? x : 0;
+      tot += x;
+    }
+    wx_i64 item = s_items + wb + incl - nch;
+    for (wx_i64 c = 0; c < nch; ++c, ++item) {
+      const wx_i64 cs = st + c * a.chunk;
+      const wx_i64 cl = (len - c * a.chunk) < a.chunk ? (len - c * a.chunk) : a.chunk;
+      if (item < a.work_cap) {
+        a.work[2 * item] = ((wx_i64)p << 40) | ((nch == 1 ? 1ll : 0ll) << 39) | cl;
+        a.work[2 * item + 1] = cs;
+      }
+    }
+    __syncthreads();
+    if (tid == 0) s_items += tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    *a.n_work = s_items < a.work_cap ? s_items : a.work_cap;
+    if (s_items > a.work_cap) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_scatter(WxGroupPartArgs wx_a) {
+  extern __shared__ wx_u32 wx_s_dyn[];
+  wx_i64 *s_base = reinterpret_cast<wx_i64 *>(wx_s_dyn);        // [P]
+  wx_u32 *s_cur = reinterpret_cast<wx_u32 *>(s_base + wx_a.n_part);  // [P]
+  for (int p = threadIdx.x; p < wx_a.n_part; p += WX_GP_BLOCK) {
+    s_base[p] = wx_a.poff[(wx_i64)p * wx_a.n_wg + blockIdx.x];
+    s_cur[p] = 0u;
+  }
+  __syncthreads();
+  const wx_i64 wx_rb = (wx_i64)blockIdx.x * wx_a.rows_per_wg;
+  const wx_i64 wx_re = wx_rb + wx_a.rows_per_wg < wx_a.n_rows ? wx_rb + wx_a.rows_per_wg : wx_a.n_rows;
+  const wx_u32 wx_bmask = (1u << wx_a.shift) - 1u;
+  {
+    WX_RANGE_LOOP_BEGIN(wx_rb, wx_re)
+    if (idx < wx_rend && WX_EVAL_COND()) {
+      const wx_u32 wx_d = (wx_u32) static_cast<int>(WX_KEY) - (wx_u32)wx_a.key_lo;
+      const wx_u32 wx_p = wx_d >> wx_a.shift;
+      const float wx_v = static_cast<float>(WX_EXPR);
+      if (wx_p < (wx_u32)wx_a.n_part) {
+        const wx_u32 r = atomicAdd(&s_cur[wx_p], 1u);
+        wx_a.pairs[s_base[wx_p] + r] = ((wx_u64)(wx_d & wx_bmask) << 32) | __float_as_uint(wx_v);
+      }
+    }
+    WX_RANGE_LOOP_END
+  }
+}
+
+#define WX_GP_AGG_BATCH 4
+extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGroupPartArgs a) {
+  extern __shared__ wx_u32 wx_s_dyn[];
+  const int B = 1 << a.shift;
+  double *s_sum = reinterpret_cast<double *>(wx_s_dyn);  // [B]
+  wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_sum + B);   // [B]
+  const wx_i64 nw = *a.n_work;
+  for (wx_i64 w = blockIdx.x; w < nw; w += gridDim.x) {
+    const wx_i64 w0 = a.work[2 * w], start = a.work[2 * w + 1];
+    const int p = (int)(w0 >> 40);
+    const bool whole = ((w0 >> 39) & 1) != 0;
+    const wx_i64 end = start + (w0 & ((1ll << 39) - 1));
+    for (int b = threadIdx.x; b < B; b += WX_GP_BLOCK) { s_sum[b] = 0.0; s_cnt[b] = 0u; }
+    __syncthreads();
+    for (wx_i64 i0 = start + threadIdx.x; i0 < end; i0 += (wx_i64)WX_GP_BLOCK * WX_GP_AGG_BATCH) {
+      wx_u64 pr[WX_GP_AGG_BATCH];
+#pragma unroll
+      for (int j = 0; j < WX_GP_AGG_BATCH; ++j) {
+        const wx_i64 i = i0 + (wx_i64)j * WX_GP_BLOCK;
+        pr[j] = i < end ? __builtin_nontemporal_load(a.pairs + i) : ~0ull;
+      }
+#pragma unroll
+      for (int j = 0; j < WX_GP_AGG_BATCH; ++j) {
+        if (pr[j] == ~0ull) continue;
+        const wx_u32 b = (wx_u32)(pr[j] >> 32);
+        atomicAdd(&s_sum[b], (double)__uint_as_float((wx_u32)pr[j]));
+        atomicAdd(&s_cnt[b], 1u);
+      }
+    }
+    __syncthreads();
+    const wx_i64 g0 = (wx_i64)p << a.shift;
+    for (int b = threadIdx.x; b < B; b += WX_GP_BLOCK) {
+      const wx_u32 c = s_cnt[b];
+      if (!c) continue;
+      if (whole) {
+        a.dsum[g0 + b] = s_sum[b];
+        a.dcnt[g0 + b] = c;
+      } else {
+        atomicAdd(&a.dsum[g0 + b], s_sum[b]);
+        atomicAdd(&a.dcnt[g0 + b], (wx_u64)c);
+      }
+    }
+    __syncthreads();
+  }
+}
+
+// non-empty keys of partition blockIdx.x
+extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_count(WxGroupPartArgs a) {
+  __shared__ wx_u32 s_n;
+  if (threadIdx.x == 0) s_n = 0u;
+  __syncthreads();
+  const int B = 1 << a.shift;
+  const wx_i64 g0 = (wx_i64)blockIdx.x << a.shift;
+  wx_u32 n = 0;
+  for (int b = threadIdx.x; b < B; b += WX_GP_BLOCK) n += a.dcnt[g0 + b] != 0ull ? 1u : 0u;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+  if ((threadIdx.x & 63) == 0) atomicAdd(&s_n, n);
+  __syncthreads();
+  if (threadIdx.x == 0) a.pnz[blockIdx.x] = s_n;
+}
+
+// exclusive prefix of the partitions' key counts in place; the total is the group count
+extern "C" __global__ __launch_bounds__(1024) void wx_group_part_scan2(WxGroupPartArgs a) {
+  __shared__ wx_i64 s_w[16];
+  const wx_i64 total = wx_block_scan_excl(a.pnz, a.pnz, (wx_i64)a.n_part, s_w);
+  if (threadIdx.x == 0) {
+    *a.n_groups_out = total;
+    if (total > a.capacity) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_CAPACITY);
+  }
+}
+
+// partition blockIdx.x's groups at their ascending-key positions; dense arrays re-zeroed
+extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_emit(WxGroupPartArgs a) {
+  __shared__ wx_u32 s_w[WX_GP_BLOCK / 64];
+  const int B = 1 << a.shift;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const wx_i64 g0 = (wx_i64)blockIdx.x << a.shift;
+  wx_i64 pos = a.pnz[blockIdx.x];
+  for (int b0 = 0; b0 < B; b0 += WX_GP_BLOCK) {
+    const int b = b0 + tid;
+    const wx_u64 c = b < B ? a.dcnt[g0 + b] : 0ull;
+    const wx_u32 f = c ? 1u : 0u;
+    const wx_u64 m = __builtin_amdgcn_ballot_w64(f != 0u);
+    if (lane == 0) s_w[wave] = (wx_u32)__builtin_popcountll(m);
+    __syncthreads();
+    wx_u32 wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WX_GP_BLOCK / 64; ++w) {
+      const wx_u32 x = s_w[w];
+      wb += w < wave ? x : 0u;
+      tot += x;
+    }
+    if (c) {
+      const wx_i64 o = pos + wb + ::wx::lanes_below(m);
+      if (o < a.capacity) {
+        a.out_keys[o] = (int)((wx_u32)a.key_lo + (wx_u32)(g0 + b));
+        a.out_sums[o] = a.dsum[g0 + b];
+        a.out_counts[o] = (wx_i64)c;
+      }
+      a.dsum[g0 + b] = 0.0;
+      a.dcnt[g0 + b] = 0ull;
+    }
+    pos += tot;
+    __syncthreads();
+  }
+}
+
 // One 1024-thread block: sort the general-key entries, merge with the dense
 // window in ascending key order, write the outputs, zero what was used.  The
 // window is two adjacent bins per thread, all loaded up front (one round trip
