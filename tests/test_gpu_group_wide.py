@@ -114,3 +114,17 @@ def test_partitioned_float_and_int64_columns():
     rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", None, capacity=1 << 22)
     assert np.array_equal(gk, rk) and np.array_equal(gc, rc)
     np.testing.assert_allclose(gs, rs, rtol=1e-9, atol=1e-9)  # float(double) values summed in double
+
+
+@pytest.mark.parametrize("guess", ["1", "0"])
+def test_partitioned_sample_misses_outliers(guess, monkeypatch):
+    """The first pass runs over a range guessed from a 65 536-row sample:
+    rare keys far outside it (never sampled) must send the query through
+    the exact-range pass, and a selective WHERE leaves the sample few rows."""
+    monkeypatch.setenv("WARPDB_GP_GUESS", guess)
+    i = np.arange(N, dtype=np.int64)
+    keys = (i * 48271) % 100_000
+    keys[[17, 900_001, N - 2]] = [3_000_000, -2_000_000, 5_000_000]  # between sampled rows
+    cols = _table(keys)
+    _check(cols)
+    _check(cols, cond="price > 39.9", lowered_cond="(price[idx] > 39.9f)")

@@ -1510,25 +1510,111 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_part_minmax(WxGr
   }
 }
 
+// Rows per partition of this workgroup's range.  With wx_a.mm set (the
+// first pass over a range guessed from a sample) it also records the exact
+// (min, max) key, the passing rows and the rows outside the guessed range
+// (mm[4g .. 4g+3]); the host keeps the counts only when there were none.
 extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_hist(WxGroupPartArgs wx_a) {
   extern __shared__ wx_u32 wx_s_dyn[];
   wx_u32 *s_h = wx_s_dyn;  // [P]
+  __shared__ int s_mn[WX_GP_BLOCK / 64], s_mx[WX_GP_BLOCK / 64];
+  __shared__ wx_u64 s_c[WX_GP_BLOCK / 64], s_o[WX_GP_BLOCK / 64];
   for (int i = threadIdx.x; i < wx_a.n_part; i += WX_GP_BLOCK) s_h[i] = 0u;
   __syncthreads();
+  const bool wx_guess = wx_a.mm != nullptr;
+  int wx_mn = 0x7fffffff, wx_mx = (int)0x80000000;
+  wx_u64 wx_c = 0, wx_o = 0;
   const wx_i64 wx_rb = (wx_i64)blockIdx.x * wx_a.rows_per_wg;
   const wx_i64 wx_re = wx_rb + wx_a.rows_per_wg < wx_a.n_rows ? wx_rb + wx_a.rows_per_wg : wx_a.n_rows;
   {
     WX_RANGE_LOOP_BEGIN(wx_rb, wx_re)
     if (idx < wx_rend && WX_EVAL_COND()) {
-      const wx_u32 wx_p = ((wx_u32) static_cast<int>(WX_KEY) - (wx_u32)wx_a.key_lo) >> wx_a.shift;
-      if (wx_p < (wx_u32)wx_a.n_part) atomicAdd(&s_h[wx_p], 1u);
+      const int wx_k = static_cast<int>(WX_KEY);
+      const wx_u32 wx_p = ((wx_u32)wx_k - (wx_u32)wx_a.key_lo) >> wx_a.shift;
+      if (wx_guess) {
+        wx_mn = wx_k < wx_mn ? wx_k : wx_mn;
+        wx_mx = wx_k > wx_mx ? wx_k : wx_mx;
+        ++wx_c;
+      }
+      if (wx_p < (wx_u32)wx_a.n_part && wx_k >= wx_a.key_lo) atomicAdd(&s_h[wx_p], 1u);
+      else if (wx_guess) ++wx_o;
       else atomicOr(reinterpret_cast<unsigned int *>(&wx_a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
     }
     WX_RANGE_LOOP_END
   }
+  if (wx_guess) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int a = __shfl_xor(wx_mn, o), b = __shfl_xor(wx_mx, o);
+      wx_mn = a < wx_mn ? a : wx_mn;
+      wx_mx = b > wx_mx ? b : wx_mx;
+      wx_c += __shfl_xor(wx_c, o);
+      wx_o += __shfl_xor(wx_o, o);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      const int w = threadIdx.x >> 6;
+      s_mn[w] = wx_mn; s_mx[w] = wx_mx; s_c[w] = wx_c; s_o[w] = wx_o;
+    }
+  }
   __syncthreads();
   for (int p = threadIdx.x; p < wx_a.n_part; p += WX_GP_BLOCK)
     wx_a.pcount[(wx_i64)p * wx_a.n_wg + blockIdx.x] = s_h[p];
+  if (wx_guess && threadIdx.x == 0) {
+    for (int w = 1; w < WX_GP_BLOCK / 64; ++w) {
+      wx_mn = s_mn[w] < wx_mn ? s_mn[w] : wx_mn;
+      wx_mx = s_mx[w] > wx_mx ? s_mx[w] : wx_mx;
+      wx_c += s_c[w];
+      wx_o += s_o[w];
+    }
+    wx_a.mm[4 * blockIdx.x] = wx_mn;
+    wx_a.mm[4 * blockIdx.x + 1] = wx_mx;
+    wx_a.mm[4 * blockIdx.x + 2] = (wx_i64)wx_c;
+    wx_a.mm[4 * blockIdx.x + 3] = (wx_i64)wx_o;
+  }
+}
+
+// A strided sample of the rows (thread i: row i * n / S): the (min, max) key
+// and passing rows per workgroup, from which the host guesses the range of
+// the first pass (mm[3g .. 3g+2]).
+extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_sample(WxGroupPartArgs wx_a) {
+  __shared__ int s_mn[WX_GP_BLOCK / 64], s_mx[WX_GP_BLOCK / 64];
+  __shared__ wx_u64 s_c[WX_GP_BLOCK / 64];
+  int wx_mn = 0x7fffffff, wx_mx = (int)0x80000000;
+  wx_u64 wx_c = 0;
+  const wx_i64 wx_s = (wx_i64)gridDim.x * WX_GP_BLOCK;
+  const wx_i64 wx_i = (wx_i64)blockIdx.x * WX_GP_BLOCK + threadIdx.x;
+  if (wx_a.n_rows > 0) {
+    const wx_i64 idx = wx_i * (wx_a.n_rows / wx_s) + (wx_i * (wx_a.n_rows % wx_s)) / wx_s;  // i * n / S
+    WX_COLS(WX_BIND_ROW)
+    if (WX_EVAL_COND()) {
+      const int wx_k = static_cast<int>(WX_KEY);
+      wx_mn = wx_k;
+      wx_mx = wx_k;
+      wx_c = 1;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const int a = __shfl_xor(wx_mn, o), b = __shfl_xor(wx_mx, o);
+    wx_mn = a < wx_mn ? a : wx_mn;
+    wx_mx = b > wx_mx ? b : wx_mx;
+    wx_c += __shfl_xor(wx_c, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    s_mn[w] = wx_mn; s_mx[w] = wx_mx; s_c[w] = wx_c;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < WX_GP_BLOCK / 64; ++w) {
+      wx_mn = s_mn[w] < wx_mn ? s_mn[w] : wx_mn;
+      wx_mx = s_mx[w] > wx_mx ? s_mx[w] : wx_mx;
+      wx_c += s_c[w];
+    }
+    wx_a.mm[3 * blockIdx.x] = wx_mn;
+    wx_a.mm[3 * blockIdx.x + 1] = wx_mx;
+    wx_a.mm[3 * blockIdx.x + 2] = (wx_i64)wx_c;
+  }
 }
 
 // Exclusive scan of a device array of n values (one 1024-thread block, 4
@@ -1653,6 +1739,131 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_scatter(
   }
 }
 
+// Staged scatter (P <= WX_GP_STAGE_MAXP): each tile of WX_GP_BLOCK x 4 x
+// WX_GP_SUNROLL rows is counting-sorted by partition in LDS (ds_add_rtn
+// ranks, a block scan of the tile's per-partition counts), then written out
+// so that consecutive threads store consecutive slots of one partition's
+// run.  Software-pipelined: the next tile's column loads are issued as soon
+// as this tile's rows are evaluated, so they are in flight during the LDS
+// phases.  The direct form above stores 8 bytes per lane to P different
+// places: 1.5 TB/s at 1e9 rows; staged without the pipelining 3.0-3.4 TB/s.
+#define WX_GP_STAGE_MAXP 2048
+#ifndef WX_GP_SUNROLL
+#define WX_GP_SUNROLL 4  // row quads per thread per staged tile (the host sizes the LDS to match)
+#endif
+#define WX_GP_TILE (WX_GP_BLOCK * 4 * WX_GP_SUNROLL)
+#define WX_GP_SSPAN ((wx_i64)WX_GP_BLOCK * WX_GP_SUNROLL)
+#define WX_DECL_GS(name, T, slot) T wx_u##slot[WX_GP_SUNROLL][4];
+#define WX_LOAD_GS(name, T, slot) ::wx::load4_tail<T>(wx_a.col[slot], wx_r0u, wx_rend, wx_u##slot[wx_u]);
+extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_scatter_lds(WxGroupPartArgs wx_a) {
+  extern __shared__ wx_u32 wx_s_dyn[];
+  wx_u64 *s_pair = reinterpret_cast<wx_u64 *>(wx_s_dyn);          // [WX_GP_TILE] (p << 45 | bin << 32 | value)
+  wx_i64 *s_gbase = reinterpret_cast<wx_i64 *>(s_pair + WX_GP_TILE);  // [P] next global slot of (p, this workgroup)
+  wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_gbase + wx_a.n_part);  // [P] this tile's rows of p
+  wx_u32 *s_start = s_cnt + wx_a.n_part;                              // [P] first LDS slot of p
+  __shared__ wx_u32 s_w[WX_GP_BLOCK / 64];
+  const int P = wx_a.n_part;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int p = tid; p < P; p += WX_GP_BLOCK) {
+    s_gbase[p] = wx_a.poff[(wx_i64)p * wx_a.n_wg + blockIdx.x];
+    s_cnt[p] = 0u;
+  }
+  const wx_i64 wx_rb = (wx_i64)blockIdx.x * wx_a.rows_per_wg;
+  const wx_i64 wx_re = wx_rb + wx_a.rows_per_wg < wx_a.n_rows ? wx_rb + wx_a.rows_per_wg : wx_a.n_rows;
+  const wx_u32 wx_bmask = (1u << wx_a.shift) - 1u;
+  const wx_i64 wx_rend = wx_re;
+  const wx_i64 wx_qe = (wx_rend + 3) >> 2, wx_qfull = wx_rend >> 2;
+  WX_COLS(WX_DECL_GS)
+  wx_i64 wx_base = wx_rb >> 2;
+  // one tile's loads into the column registers (unguarded when whole)
+#define WX_GS_LOAD_TILE()                                                        \
+  if (WX_ALIGNED16 && wx_base + WX_GP_SSPAN <= wx_qfull) {                       \
+    _Pragma("unroll") for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u) {        \
+      const wx_i64 wx_r0u = WX_GP_QUAD(wx_u) << 2;                               \
+      WX_COLS(WX_LOAD_GP_FAST)                                                   \
+    }                                                                            \
+  } else if (wx_base < wx_qe) {                                                  \
+    _Pragma("unroll") for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u) {        \
+      const wx_i64 wx_r0u = WX_GP_QUAD(wx_u) << 2;                               \
+      WX_COLS(WX_LOAD_GS)                                                        \
+    }                                                                            \
+  }
+  WX_GS_LOAD_TILE()
+  __syncthreads();
+  for (; wx_base < wx_qe; wx_base += WX_GP_SSPAN) {
+    wx_u64 wx_pr[WX_GP_SUNROLL][4];
+    wx_u32 wx_rk[WX_GP_SUNROLL][4];
+#pragma unroll
+    for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u) {
+      const wx_i64 wx_r0 = WX_GP_QUAD(wx_u) << 2;
+#pragma unroll
+      for (int wx_e = 0; wx_e < 4; ++wx_e) {
+        WX_COLS(WX_BIND_U)
+        const wx_i64 idx = wx_r0 + wx_e;
+        wx_pr[wx_u][wx_e] = ~0ull;
+        if (idx < wx_rend && WX_EVAL_COND()) {
+          const wx_u32 wx_d = (wx_u32) static_cast<int>(WX_KEY) - (wx_u32)wx_a.key_lo;
+          const wx_u32 wx_p = wx_d >> wx_a.shift;
+          const float wx_v = static_cast<float>(WX_EXPR);
+          if (wx_p < (wx_u32)P) {
+            wx_pr[wx_u][wx_e] = ((wx_u64)wx_p << 45) | ((wx_u64)(wx_d & wx_bmask) << 32) | __float_as_uint(wx_v);
+            wx_rk[wx_u][wx_e] = atomicAdd(&s_cnt[wx_p], 1u);
+          }
+        }
+      }
+    }
+    {  // the next tile's loads, in flight during this tile's LDS phases
+      const wx_i64 wx_cur = wx_base;
+      wx_base += WX_GP_SSPAN;
+      WX_GS_LOAD_TILE()
+      wx_base = wx_cur;
+    }
+    __syncthreads();
+    // exclusive scan of the tile's per-partition counts (P <= 2048: two per thread)
+    const wx_u32 c0 = 2 * tid < P ? s_cnt[2 * tid] : 0u, c1 = 2 * tid + 1 < P ? s_cnt[2 * tid + 1] : 0u;
+    wx_u32 incl = c0 + c1;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_u32 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    wx_u32 wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WX_GP_BLOCK / 64; ++w) {
+      const wx_u32 x = s_w[w];
+      wb += w < wave ? x : 0u;
+      tot += x;
+    }
+    const wx_u32 ex = wb + incl - c0 - c1;
+    if (2 * tid < P) s_start[2 * tid] = ex;
+    if (2 * tid + 1 < P) s_start[2 * tid + 1] = ex + c0;
+    __syncthreads();
+#pragma unroll
+    for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u)
+#pragma unroll
+      for (int wx_e = 0; wx_e < 4; ++wx_e)
+        if (wx_pr[wx_u][wx_e] != ~0ull) {
+          const wx_u32 p = (wx_u32)(wx_pr[wx_u][wx_e] >> 45);
+          s_pair[s_start[p] + wx_rk[wx_u][wx_e]] = wx_pr[wx_u][wx_e];
+        }
+    __syncthreads();
+    for (wx_u32 j = tid; j < tot; j += WX_GP_BLOCK) {
+      const wx_u64 e = s_pair[j];
+      const wx_u32 p = (wx_u32)(e >> 45);
+      wx_a.pairs[s_gbase[p] + (j - s_start[p])] = e & 0x00001fffffffffffull;
+    }
+    __syncthreads();
+    for (int p = tid; p < P; p += WX_GP_BLOCK) {  // owner thread: advance the runs, clear the counts
+      s_gbase[p] += s_cnt[p];
+      s_cnt[p] = 0u;
+    }
+    __syncthreads();
+  }
+#undef WX_GS_LOAD_TILE
+}
+
 #define WX_GP_AGG_BATCH 4
 extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGroupPartArgs a) {
   extern __shared__ wx_u32 wx_s_dyn[];
@@ -1667,19 +1878,34 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGr
     const wx_i64 end = start + (w0 & ((1ll << 39) - 1));
     for (int b = threadIdx.x; b < B; b += WX_GP_BLOCK) { s_sum[b] = 0.0; s_cnt[b] = 0u; }
     __syncthreads();
-    for (wx_i64 i0 = start + threadIdx.x; i0 < end; i0 += (wx_i64)WX_GP_BLOCK * WX_GP_AGG_BATCH) {
-      wx_u64 pr[WX_GP_AGG_BATCH];
+    // 16-byte loads (two pairs per lane) over the even-aligned middle; the
+    // odd head and tail pair, if any, by threads 0 and 1
+    const wx_i64 q0 = (start + 1) >> 1, q1 = end >> 1;
+    if (threadIdx.x < 2) {
+      const wx_i64 i = threadIdx.x == 0 ? start : (q1 << 1);
+      const bool take = threadIdx.x == 0 ? (start & 1) && start < end : (end & 1) && (q1 << 1) >= start && q1 >= q0;
+      if (take) {
+        const wx_u64 pr = a.pairs[i];
+        atomicAdd(&s_sum[(wx_u32)(pr >> 32)], (double)__uint_as_float((wx_u32)pr));
+        atomicAdd(&s_cnt[(wx_u32)(pr >> 32)], 1u);
+      }
+    }
+    typedef wx_u64 wx_u64x2 __attribute__((ext_vector_type(2)));
+    const wx_u64x2 *pv = reinterpret_cast<const wx_u64x2 *>(a.pairs);
+    for (wx_i64 j0 = q0 + threadIdx.x; j0 < q1; j0 += (wx_i64)WX_GP_BLOCK * WX_GP_AGG_BATCH) {
+      wx_u64x2 pr[WX_GP_AGG_BATCH];
 #pragma unroll
       for (int j = 0; j < WX_GP_AGG_BATCH; ++j) {
-        const wx_i64 i = i0 + (wx_i64)j * WX_GP_BLOCK;
-        pr[j] = i < end ? __builtin_nontemporal_load(a.pairs + i) : ~0ull;
+        const wx_i64 q = j0 + (wx_i64)j * WX_GP_BLOCK;
+        pr[j] = q < q1 ? __builtin_nontemporal_load(pv + q) : wx_u64x2{~0ull, ~0ull};
       }
 #pragma unroll
       for (int j = 0; j < WX_GP_AGG_BATCH; ++j) {
-        if (pr[j] == ~0ull) continue;
-        const wx_u32 b = (wx_u32)(pr[j] >> 32);
-        atomicAdd(&s_sum[b], (double)__uint_as_float((wx_u32)pr[j]));
-        atomicAdd(&s_cnt[b], 1u);
+        if (pr[j].x == ~0ull) continue;
+        atomicAdd(&s_sum[(wx_u32)(pr[j].x >> 32)], (double)__uint_as_float((wx_u32)pr[j].x));
+        atomicAdd(&s_cnt[(wx_u32)(pr[j].x >> 32)], 1u);
+        atomicAdd(&s_sum[(wx_u32)(pr[j].y >> 32)], (double)__uint_as_float((wx_u32)pr[j].y));
+        atomicAdd(&s_cnt[(wx_u32)(pr[j].y >> 32)], 1u);
       }
     }
     __syncthreads();

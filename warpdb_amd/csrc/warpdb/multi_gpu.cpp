@@ -310,7 +310,9 @@ struct GroupScratch {
 
 // Per-shard top-K candidates and their all-gathered copies (k <= 32).
 struct TopkScratch {
-  DeviceBuffer cand, all;  // [keys f32 x 32 | vals f32 x 32 | rows i64 x 32 | count i64], x shards for `all`
+  // wx_topk_record: [keys f32 x 32 | vals f32 x 32 | rows i64 x 32 | count i64], x shards for `all`;
+  // `out` the merged global top-K in the same layout
+  DeviceBuffer cand, all, out;
   int shards = 0;
 };
 constexpr size_t kTopkMax = 32;
@@ -428,9 +430,9 @@ std::vector<float> ResidentShards::dense(const std::string &expr_cuda, const std
 }
 
 // ORDER BY .. LIMIT k over the shards: wx_topk per device
-// (global row numbers via the shard's row base) into one packed record,
-// ONE ncclAllGather of the records (bytes), then the (key, row) merge of
-// the <= 32 x shards candidates on the host.
+// (global row numbers via the shard's row base) into one wx_topk_record,
+// ONE ncclAllGather of the records (bytes), then wx_topk_merge of the
+// <= 32 x shards candidates on the first shard's device.
 TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string &cond_cuda,
                                 const std::string &select_cuda, int k, bool descending) const {
   if (k < 1 || k > static_cast<int>(kTopkMax)) throw std::runtime_error("top-K supports 1 <= k <= 32");
@@ -486,49 +488,39 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
     }
     if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("RCCL all-gather failed");
   }
+  // the global top-K on the first shard's device: wx_topk_merge over the
+  // gathered records (better key, NaN last, then the smaller row), k results
+  // read back with the count
+  TopkScratch &t0 = impl_->topk[0];
+  const int dev0 = ranges[0].device;
+  if (!t0.out.ptr) t0.out = DeviceBuffer(dev0, kTopkRec);
+  char *o = static_cast<char *>(t0.out.ptr);
   char err[1024];
+  {
+    DevGuard dg(dev0);
+    wx_launch L = sync_launch(dev0, streams[0]);
+    L.flags = 0;
+    throw_on(wx_topk_merge(static_cast<const wx_topk_record *>(ns > 1 ? t0.all.ptr : t0.cand.ptr),
+                           static_cast<int32_t>(ns), k, descending ? 1 : 0, &L, reinterpret_cast<float *>(o),
+                           reinterpret_cast<int64_t *>(o + kTopkMax * 8), reinterpret_cast<float *>(o + kTopkMax * 4),
+                           reinterpret_cast<int64_t *>(o + kTopkMax * 16), nullptr, err, sizeof(err)),
+             err);
+  }
   for (size_t i = 0; i < ns; ++i) {
     DevGuard dg(ranges[i].device);
     hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
     wx_launch L = sync_launch(ranges[i].device, streams[i]);
     throw_on(wx_check(&L, err, sizeof(err)), err);
   }
-  std::vector<char> h(kTopkRec * ns);
+  wx_topk_record h;
   {
-    DevGuard dg(ranges[0].device);
-    const void *src = ns > 1 ? impl_->topk[0].all.ptr : impl_->topk[0].cand.ptr;
-    hip_ok(hipMemcpy(h.data(), src, h.size(), hipMemcpyDeviceToHost), "hipMemcpy");
+    DevGuard dg(dev0);
+    hip_ok(hipMemcpy(&h, o, sizeof(h), hipMemcpyDeviceToHost), "hipMemcpy");
   }
-  struct Cand {
-    float key, val;
-    int64_t row;
-  };
-  std::vector<Cand> cand;
-  for (size_t i = 0; i < ns; ++i) {
-    const char *rec = h.data() + i * kTopkRec;
-    int64_t m = 0;
-    std::memcpy(&m, rec + kTopkMax * 16, 8);
-    for (int64_t j = 0; j < m; ++j) {
-      Cand c;
-      std::memcpy(&c.key, rec + 4 * j, 4);
-      std::memcpy(&c.val, rec + kTopkMax * 4 + 4 * j, 4);
-      std::memcpy(&c.row, rec + kTopkMax * 8 + 8 * j, 8);
-      cand.push_back(c);
-    }
-  }
-  // better key first (NaN last either way, -0.0 == +0.0), then the smaller row
-  auto better = [descending](const Cand &a, const Cand &b) {
-    const bool na = std::isnan(a.key), nb = std::isnan(b.key);
-    if (na != nb) return nb;
-    if (!na && a.key != b.key) return descending ? a.key > b.key : a.key < b.key;
-    return a.row < b.row;
-  };
-  std::sort(cand.begin(), cand.end(), better);
-  if (cand.size() > static_cast<size_t>(k)) cand.resize(k);
-  for (const Cand &c : cand) {
-    res.keys.push_back(c.key);
-    res.rows.push_back(c.row);
-    res.values.push_back(c.val);
+  for (int64_t j = 0; j < h.count; ++j) {
+    res.keys.push_back(h.keys[j]);
+    res.rows.push_back(h.rows[j]);
+    res.values.push_back(h.vals[j]);
   }
   return res;
 }
