@@ -13,6 +13,9 @@ computed:
   workload_c3.npz  SUM(price) GROUP BY quantity (int32 keys 0..1023),
                    100 000 rows: the reference query_sql's std::map
                    aggregation in double (src/warpdb.cpp:375-385)
+  workload_c3w.npz SUM(price) GROUP BY quantity with int32 keys over
+                   0..74 999 (about 55 000 distinct in 100 000 rows): the
+                   many-key GROUP BY, same std::map aggregation
   workload_c5.npz  ORDER BY price DESC LIMIT 32 over 100 000 rows of
                    price rounded to 0.25 (heavy ties): rows + key bits of a
                    stable sort by the reference's eval_node value
@@ -56,6 +59,12 @@ def csv_text(cols: dict, int_cols=()) -> str:
     return "\n".join(lines) + "\n"
 
 
+def c3w_table(n: int):
+    """price f32 U[0,40), quantity int32 U{0..74999}: many distinct keys."""
+    return {"price": synth.uniform_f32(n, synth.SEED_PRICE, 0.0, 40.0),
+            "quantity": synth.uniform_int(n, synth.SEED_KEY, 0, 74_999).astype(np.int32)}
+
+
 def c5_table(n: int):
     """price U[0,40) rounded to multiples of 0.25: ~160 distinct keys, heavy ties."""
     p = synth.uniform_f32(n, synth.SEED_PRICE, 0.0, 40.0)
@@ -77,6 +86,7 @@ def main():
             "c2": (synth.c2_table(N), (), None, "price * quantity WHERE price > 15"),
             "c4": (synth.c2_table(N), (), None, "price * 0.9 WHERE price > 20"),
             "c3": (synth.c3_table(N), ("quantity",), "20", None),
+            "c3w": (c3w_table(N), ("quantity",), "20", None),
             "c5": (c5_table(N), (), None, None),
         }
         for name, (cols, ints, schema, query) in tables.items():
@@ -94,13 +104,14 @@ def main():
                 np.savez_compressed(os.path.join(HERE, f"workload_{name}.npz"), mask=np.packbits(mask),
                                     bits=vals.view(np.uint32))
                 case.update(query=query, generator="synth.c2_table", passing=int(len(idx)))
-            elif name == "c3":
+            elif name in ("c3", "c3w"):
                 rows = [ln.split() for ln in run("groupsum", path, "price", "quantity", schema).splitlines()]
-                np.savez_compressed(os.path.join(HERE, "workload_c3.npz"),
+                np.savez_compressed(os.path.join(HERE, f"workload_{name}.npz"),
                                     keys=np.array([int(r[0]) for r in rows], np.int32),
                                     sums=np.array([float.fromhex(r[1]) for r in rows], np.float64),
                                     counts=np.array([int(r[2]) for r in rows], np.int64))
-                case.update(query="SELECT SUM(price) FROM t GROUP BY quantity", generator="synth.c3_table",
+                case.update(query="SELECT SUM(price) FROM t GROUP BY quantity",
+                            generator="synth.c3_table" if name == "c3" else "make_workload_golden.c3w_table",
                             groups=len(rows))
             else:
                 rows = [ln.split() for ln in run("topk", path, "price", "32", "1").splitlines()]

@@ -39,6 +39,8 @@ def table(name):
         return synth.c2_table(N), ()
     if name == "c3":
         return synth.c3_table(N), ("quantity",)
+    if name == "c3w":
+        return mk.c3w_table(N), ("quantity",)
     return mk.c5_table(N), ()
 
 
@@ -52,7 +54,7 @@ def compaction_fixture(name):
     return idx, f["bits"]
 
 
-@pytest.mark.parametrize("name", ["c2", "c3", "c4", "c5"])
+@pytest.mark.parametrize("name", ["c2", "c3", "c3w", "c4", "c5"])
 def test_regenerated_table_is_the_reference_input(name):
     cols, ints = table(name)
     text = mk.csv_text(cols, ints)
@@ -70,10 +72,12 @@ def test_oracle_equals_reference_compaction(name):
     assert np.array_equal(vals.view(np.uint32), rbits)
 
 
-def test_oracle_equals_reference_group_by():
-    cols, _ = table("c3")
+@pytest.mark.parametrize("name", ["c3", "c3w"])
+def test_oracle_equals_reference_group_by(name):
+    cols, _ = table(name)
     k, s, c = ora.group_sum(ora.HostTable(cols), "price", "quantity", sem=ora.SEM_CPU)
-    f = fixture("c3")
+    f = fixture(name)
+    assert len(k) == META["cases"][name]["groups"]
     assert np.array_equal(k, f["keys"]) and np.array_equal(c, f["counts"])
     assert np.array_equal(s, f["sums"])  # double sums of float values: exact here
 
@@ -140,6 +144,33 @@ def test_hip_group_by_equals_reference():
     assert g == len(f["keys"])
     assert np.array_equal(keys[:g].cpu().numpy(), f["keys"]) and np.array_equal(cnts[:g].cpu().numpy(), f["counts"])
     assert np.array_equal(sums[:g].cpu().numpy(), f["sums"])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["window+hash", "partitioned"])
+def test_hip_many_key_group_by_equals_reference(path, monkeypatch):
+    """55 313 groups over 100 000 rows (keys 0..74 999), the reference's
+    std::map sums: the window + global-hash path (device-wide key sort of the
+    out-of-window groups) and the range-partitioned kernels (forced at this
+    size by the WARPDB_GP_MIN_ROWS test hook)."""
+    torch = pytest.importorskip("torch")
+    from test_gpu_parity import dev_table, launch
+    from warpdb_amd import _warpexec as wx
+
+    if path == "partitioned":
+        monkeypatch.setenv("WARPDB_GP_MIN_ROWS", "0")
+    cols, _ = table("c3w")
+    t, _ = dev_table(cols)
+    cap = 1 << 17
+    keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+    sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+    g = wx.group_sum(t, "price[idx]", "quantity[idx]", None, launch(), 0, cap, keys.data_ptr(), sums.data_ptr(),
+                     cnts.data_ptr())
+    f = fixture("c3w")
+    assert g == len(f["keys"]) == 55_313
+    assert np.array_equal(keys[:g].cpu().numpy(), f["keys"]) and np.array_equal(cnts[:g].cpu().numpy(), f["counts"])
+    assert np.array_equal(sums[:g].cpu().numpy(), f["sums"])  # few rows per key: exact in any order
 
 
 @pytest.mark.gpu
