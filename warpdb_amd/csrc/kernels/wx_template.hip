@@ -3154,6 +3154,8 @@ struct WxRsShared {
   wx_u32 wc[WX_RS_WAVES][256];  // per-wave digit counts, then their exclusive prefix over the waves
   wx_u32 gb[256];  // output slot of digit d's first key minus its tile-local offset
   wx_u32 ld[256];  // tile-local exclusive prefix of the digit counts
+  wx_u32 tt[256];  // the tile's count of digit d (paired look-back)
+  wx_u32 inc[256];  // its wave-inclusive prefix over the digits (paired look-back)
   wx_u32 wsum[4];
   wx_u32 tk[2];  // tile ticket
 };
@@ -3453,6 +3455,136 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
   }
 }
 
+#ifndef WX_RS_LB_PAIR
+// Paired look-back (key tiles): digit d's walk is shared by lanes 2d and
+// 2d + 1 of the whole 512-thread tile (waves 4-7 used to idle through it),
+// each loading WX_RS_LBW predecessor words per round -- half 0 the nearer,
+// half 1 the next ones -- and combining their partial results with one
+// lane shuffle, so a round covers 2 x WX_RS_LBW predecessors at the
+// registers of WX_RS_LBW (128 VGPRs, no spill).  Correct, and slower: 14.60
+// vs 13.72 ms per 1e9 float keys in one process, three alternating rounds
+// (profiles/r03/abl_sort_lbpair.txt) -- the walk waits on predecessors that
+// have not published yet far more than it walks published ones, and the
+// doubled poll traffic costs more than the halved round count saves.  Off.
+#define WX_RS_LB_PAIR 0
+#endif
+// As wx_rs_digits, with the look-back of digit tid >> 1 on lane pair
+// (tid & ~1, tid | 1): every thread of the tile holds this function's barrier.
+__device__ __forceinline__ void wx_rs_digits_pair(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const wx_u64 E = (wx_u64)a.epoch << 58;
+  const bool look = tile != 0 && !WX_RS_DIAG_NO_LOOKBACK;
+  if (tid < 256) {
+    wx_u32 tot = 0u;
+#pragma unroll
+    for (int w = 0; w < WX_RS_WAVES; ++w) {
+      const wx_u32 c = S.wc[w][tid];
+      S.wc[w][tid] = tot;
+      tot += c;
+    }
+    wx::st_agent(&a.status[(wx_u64)tile * 256 + tid], E | (look ? WX_RS_FLAG_A : WX_RS_FLAG_P) | tot);
+    wx_u32 inc = tot;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_u32 t = __shfl_up(inc, o);
+      if (lane >= o) inc += t;
+    }
+    if (lane == 63) S.wsum[wave] = inc;
+    S.tt[tid] = tot;
+    S.inc[tid] = inc;
+  }
+  const int d = tid >> 1, h = tid & 1;
+  // this half's first round, in flight across the barrier
+  wx_i64 p = (wx_i64)tile - 1;
+  wx_u64 wv[WX_RS_LBW];
+#pragma unroll
+  for (int j = 0; j < WX_RS_LBW; ++j) {
+    const wx_i64 q = p - h * WX_RS_LBW - j;
+    wv[j] = (look && q >= 0) ? wx::ld_agent(&a.status[(wx_u64)q * 256 + d]) : (E | WX_RS_FLAG_P);
+  }
+  __syncthreads();
+  wx_u64 excl = 0;
+  if (look) {
+    wx_u32 spins = 0;
+    wx_u64 t_last = 0ull;
+    bool fresh = true;
+    while (true) {
+      if (!fresh) {
+#pragma unroll
+        for (int j = 0; j < WX_RS_LBW; ++j) {
+          const wx_i64 q = p - h * WX_RS_LBW - j;
+          wv[j] = q >= 0 ? wx::ld_agent(&a.status[(wx_u64)q * 256 + d]) : (E | WX_RS_FLAG_P);
+        }
+      }
+      fresh = false;
+      // this half: index of its first unpublished word, whether a {P} comes
+      // before it, the sum up to either
+      int stop = WX_RS_LBW;
+      bool done = false;
+      wx_u64 sum = 0;
+#pragma unroll
+      for (int j = 0; j < WX_RS_LBW; ++j) {
+        if (stop == WX_RS_LBW && !done) {
+          const wx_u64 flag = (wv[j] >> 56) & 3ull;
+          if ((wv[j] >> 58) != (wx_u64)a.epoch || flag == 0ull) {
+            stop = j;
+          } else {
+            sum += wv[j] & WX_RS_VAL_MASK;
+            done = flag == 2ull;
+          }
+        }
+      }
+      const int o_stop = __shfl_xor(stop, 1);
+      const int o_done = __shfl_xor((int)done, 1);
+      const wx_u64 o_sum = __shfl_xor(sum, 1);
+      // near = half 0's words, far = half 1's
+      const int n_stop = h ? o_stop : stop, f_stop = h ? stop : o_stop;
+      const bool n_done = h ? o_done != 0 : done, f_done = h ? done : o_done != 0;
+      const wx_u64 n_sum = h ? o_sum : sum, f_sum = h ? sum : o_sum;
+      excl += n_sum;
+      int adv;  // predecessors consumed this round
+      bool fin = false;
+      if (n_stop < WX_RS_LBW) {
+        adv = n_stop;
+      } else if (n_done) {
+        fin = true;
+        adv = 0;
+      } else {
+        excl += f_sum;
+        if (f_stop < WX_RS_LBW) adv = WX_RS_LBW + f_stop;
+        else if (f_done) { fin = true; adv = 0; }
+        else adv = 2 * WX_RS_LBW;
+      }
+      if (fin) break;
+      p -= adv;
+      if (adv == 2 * WX_RS_LBW) {
+        t_last = 0ull;  // progress
+        continue;
+      }
+      if (adv > 0) t_last = 0ull;
+      __builtin_amdgcn_s_sleep(1);
+      if ((++spins & 63u) == 0u) {
+        const wx_u64 now = __builtin_amdgcn_s_memrealtime();
+        if (t_last == 0ull) {
+          t_last = now;
+        } else if (now - t_last > WX_STALL_TICKS) {
+          atomicOr(a.err, WX_DEVERR_LOOKBACK);
+          atomicExch(&a.ctl[1], 1u);
+        }
+        if (__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+      }
+    }
+  }
+  if (h == 0) {
+    const wx_u32 tot = S.tt[d];
+    wx_u32 ld = S.inc[d] - tot;
+    for (int w = 0; w < (d >> 6); ++w) ld += S.wsum[w];
+    if (look) wx::st_agent(&a.status[(wx_u64)tile * 256 + d], E | WX_RS_FLAG_P | (excl + tot));
+    S.gb[d] = a.digit_base[d] + (wx_u32)excl - ld;
+    S.ld[d] = ld;
+  }
+}
+
 #ifndef WX_RS_SPLIT
 // 1: the keys (and payloads) are permuted into LDS by their tile-local
 // slots, which need only this tile's counts, before the look-back resolves
@@ -3653,7 +3785,10 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
     wx_rs_scatter<KIND, ASC>(a, S, wb, x, rk, pos, s_k);
     if (tid < 256) wx_rs_resolve(a, S, tile, tot, first);
   } else {
-    wx_rs_digits(a, S, tile);
+    if (WX_RS_LB_PAIR && !PAY && WX_RS_BLOCK == 512)
+      wx_rs_digits_pair(a, S, tile);
+    else
+      wx_rs_digits(a, S, tile);
     __syncthreads();
     wx_rs_scatter<KIND, ASC>(a, S, wb, x, rk, pos, s_k);
   }
