@@ -935,8 +935,16 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #define WX_TICKET_PAIR 1
 #endif
 #if defined(WX_COMPACT_STATIC) && WX_COMPACT_STATIC == 3
+#ifndef WX_DIAG_TIMELINE
+#define WX_DIAG_TIMELINE 0  // diagnostic: per-workgroup entry / first-tile / loop-end times (diag[b * 16 ..])
+#endif
 extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx_project_compact_deep(WxCompactArgs wx_a) {
   const wx_u64 wx_E = (wx_u64)wx_a.epoch << WX_EPOCH_SHIFT;
+#if WX_DIAG_TIMELINE
+  const wx_u64 wx_t_entry = __builtin_amdgcn_s_memrealtime();
+  wx_u64 wx_t_first = 0, wx_t_eval0 = 0;
+  wx_u32 wx_ntiles = 0;
+#endif
   __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
   __shared__ float s_val[2][WX_TILE];
   __shared__ unsigned short s_off[2][WX_TILE];
@@ -956,6 +964,9 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     }
   }
   __syncthreads();
+#if WX_DIAG_TIMELINE
+  wx_t_first = __builtin_amdgcn_s_memrealtime();
+#endif
   wx_i64 tile = s_tiles[0];
   wx_i64 tile1 = -1, tile2 = -1;   // tiles of iterations k - 1 and k - 2
   wx_u32 tot1 = 0, tot2 = 0;       // their passing counts
@@ -993,6 +1004,10 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
           wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
         }
       }
+#if WX_DIAG_TIMELINE
+      if (k == 0) wx_t_eval0 = __builtin_amdgcn_s_memrealtime();
+      ++wx_ntiles;
+#endif
       if (next_tile < wx_a.n_tiles) {
         const wx_i64 wx_tb = next_tile * WX_TILE;
 #pragma unroll
@@ -1114,6 +1129,16 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     tot1 = have ? block_total : 0u;
     tile = next_tile;
   }
+#if WX_DIAG_TIMELINE
+  if (tid == 0 && wx_a.diag) {
+    wx_u64 *d = wx_a.diag + (wx_u64)blockIdx.x * 16;
+    d[0] = wx_t_entry;
+    d[1] = wx_t_first;
+    d[2] = wx_t_eval0;
+    d[3] = __builtin_amdgcn_s_memrealtime();
+    d[4] = wx_ntiles;
+  }
+#endif
   if (tid == 0) wx_retire(wx_a.ctrs);
 }
 #endif
