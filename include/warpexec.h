@@ -29,6 +29,11 @@
  *   wx_group_combine    partials in an all-reduce layout and the final merge;
  *                       the reference's multi-GPU path gathers dense results
  *                       on the host instead (src/multi_gpu_utils.cpp:5-63)
+ *   wx_group_partials_slots,  the same in ONE collective: window + per-shard
+ *   wx_group_combine_slots    slots of out-of-window groups (src/multi_gpu_utils.cpp:23-60)
+ *   wx_topk_merge       ORDER BY .. LIMIT over row shards: the merge of the
+ *                       shards' candidate records (src/warpdb.cpp:453-455,
+ *                       483-495 sort the gathered dense results instead)
  *   wx_cast             device-side type conversion (jit_group_sum's float
  *                       outputs, include/jit.hpp:15-18)
  *

@@ -1359,7 +1359,10 @@ extern "C" __global__ __launch_bounds__(WX_SFIN_BLOCK) void wx_sum_finalize(WxSu
 // while every partial sum stays below 2^53 ulps of the smallest value.
 #define WX_GWIN WX_GROUP_WINDOW
 #ifndef WX_UNROLL
-#define WX_UNROLL 2
+// row quads per thread per span: 4 at 4 workgroups per CU, 1.158-1.169 vs
+// 1.177-1.182 ms per 1e9 rows for 2 (fewer workgroups per CU lose 6-85 %:
+// profiles/r03/abl_group_grid.txt)
+#define WX_UNROLL 4
 #endif
 #define WX_HSORT_MAX WX_GROUP_HSORT_MAX
 
@@ -2770,46 +2773,44 @@ extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine_sl
 extern "C" __global__ __launch_bounds__(1024) void wx_topk_merge(WxTopkMergeArgs a) {
   __shared__ wx_u32 s_r[WX_TOPK_MERGE_MAX];
   __shared__ wx_i64 s_row[WX_TOPK_MERGE_MAX];
-  __shared__ int s_src[WX_TOPK_MERGE_MAX];  // record * 32 + slot, or -1 for an unused slot
+  __shared__ float s_key[WX_TOPK_MERGE_MAX], s_val[WX_TOPK_MERGE_MAX];
+  __shared__ bool s_ok[WX_TOPK_MERGE_MAX];
   __shared__ int s_tot;
   const int tid = threadIdx.x;
   const int nc = a.n_records * a.k;
+  if (tid == 0) s_tot = 0;
   for (int c = tid; c < nc; c += 1024) {
+    // one round trip: the record's count and the slot's key, value and row
+    // are independent loads (the slot exists whether or not it is used)
     const int r = c / a.k, j = c - r * a.k;
     const unsigned char *rec = a.records + (wx_i64)r * WX_TOPK_REC_BYTES;
     const wx_i64 m = *reinterpret_cast<const wx_i64 *>(rec + WX_TOPK_MAX * 16);
-    if (j < m) {
-      const float key = reinterpret_cast<const float *>(rec)[j];
-      const wx_u32 o = wx::f2ord(key);
-      s_r[c] = (a.descending || o == 0u) ? o : ~o;  // larger is better; NaN (0) worst
-      s_row[c] = reinterpret_cast<const wx_i64 *>(rec + WX_TOPK_MAX * 8)[j];
-      s_src[c] = r * WX_TOPK_MAX + j;
-    } else {
-      s_r[c] = 0u;
-      s_row[c] = 0;
-      s_src[c] = -1;
-    }
+    const float key = reinterpret_cast<const float *>(rec)[j];
+    const float val = reinterpret_cast<const float *>(rec + WX_TOPK_MAX * 4)[j];
+    const wx_i64 row = reinterpret_cast<const wx_i64 *>(rec + WX_TOPK_MAX * 8)[j];
+    const wx_u32 o = wx::f2ord(key);
+    s_ok[c] = j < m;
+    s_r[c] = (a.descending || o == 0u) ? o : ~o;  // larger is better; NaN (0) worst
+    s_row[c] = row;
+    s_key[c] = key;
+    s_val[c] = val;
   }
-  if (tid == 0) s_tot = 0;
   __syncthreads();
   for (int c = tid; c < nc; c += 1024) {
-    const int src = s_src[c];
-    if (src < 0) continue;
+    if (!s_ok[c]) continue;
     atomicAdd(&s_tot, 1);
     const wx_u32 rc = s_r[c];
     const wx_i64 wc = s_row[c];
     int place = 0;
     for (int d = 0; d < nc; ++d) {
-      if (s_src[d] < 0 || d == c) continue;
+      if (!s_ok[d] || d == c) continue;
       const wx_u32 rd = s_r[d];
       const wx_i64 wd = s_row[d];
       place += (rd > rc || (rd == rc && (wd < wc || (wd == wc && d < c)))) ? 1 : 0;
     }
     if (place < a.k) {
-      const unsigned char *rec = a.records + (wx_i64)(src / WX_TOPK_MAX) * WX_TOPK_REC_BYTES;
-      const int j = src % WX_TOPK_MAX;
-      if (a.out_keys) a.out_keys[place] = reinterpret_cast<const float *>(rec)[j];
-      if (a.out_vals) a.out_vals[place] = reinterpret_cast<const float *>(rec + WX_TOPK_MAX * 4)[j];
+      if (a.out_keys) a.out_keys[place] = s_key[c];
+      if (a.out_vals) a.out_vals[place] = s_val[c];
       if (a.out_idx) a.out_idx[place] = wc;
     }
   }
