@@ -233,7 +233,9 @@ def roofline(bytes_per_launch, kern_ms, read_bytes, kname, traffic, timing):
             "read_only_frac": round(read_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
-def pmc_traffic(workload, n):
+def pmc_traffic(workload, n, keys=1024):
+    if workload == "group" and keys > 2048:  # the many-key (partitioned) pipeline has its own passes
+        workload = "group_wide"
     pmc = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
     if os.path.exists(pmc):
         with open(pmc) as f:
@@ -538,7 +540,7 @@ def main_ranks(args):
         line["check"] = check
         if workload == "group":
             line["config"]["distinct_keys"] = args.keys
-        line["roofline"] = roofline(bytes_per_launch, kern_avg_ms, n * rb, kname, pmc_traffic(workload, n),
+        line["roofline"] = roofline(bytes_per_launch, kern_avg_ms, n * rb, kname, pmc_traffic(workload, n, args.keys),
                                     "HIP events around the dominant kernel on its stream (max over ranks)")
     # The other north-star aggregates on the same shards, timed the same way
     # (so the driver's 1/2/4/8-GPU runs also measure SUM -- C4's 8e9 rows at

@@ -4,14 +4,16 @@
 set -euo pipefail
 W=${1:-project}
 ROWS=${2:-1e9}
+EXTRA=${3:-}   # more bench.py arguments (e.g. "--keys 1000000")
+TAG=${4:-$W}
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT=$R/gpurun_out/pmc_$W
+OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $C -d "$OUT/$C" -o run --output-format csv -- \
     python3 "$R/bench.py" --workload "$W" --rows "$ROWS" --steps 3 --warmup 1 --no-cpu-baseline --no-check \
-    --no-secondary > "$OUT/$C.log" 2>&1
+    --no-secondary $EXTRA > "$OUT/$C.log" 2>&1
 done
 python3 "$R/tools/pmc_summary.py" $(find "$OUT" -name "*counter_collection.csv") > "$OUT/summary.json"
 cat "$OUT/summary.json"
