@@ -1438,7 +1438,10 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs 
   }
   WX_STRIDE_LOOP_END
   __syncthreads();
-  for (int i = threadIdx.x; i < WX_GWIN; i += WX_BLOCK) {
+#ifndef WX_DIAG_NO_FLUSH
+#define WX_DIAG_NO_FLUSH 0  // diagnostic: the window's global flush skipped (results invalid)
+#endif
+  for (int i = threadIdx.x; i < WX_GWIN && !WX_DIAG_NO_FLUSH; i += WX_BLOCK) {
     const wx_u32 c = wx_s_cnt[i];
     if (c) {
       atomicAdd(&wx_a.win_sum[i], wx_s_sum[i]);
