@@ -13,7 +13,8 @@ import torch  # noqa: E402
 from warpdb_amd import _warpexec as wx  # noqa: E402
 
 sizes = [int(float(x)) for x in (sys.argv[1] if len(sys.argv) > 1 else "1.25e8,1e9").split(",")]
-cfgs = [c.split(":") for c in (sys.argv[2] if len(sys.argv) > 2 else "4:2,2:2,2:4,1:4,1:8,4:4").split(",")]
+# per_cu:unroll[:gblock]
+cfgs = [(c.split(":") + ["256"])[:3] for c in (sys.argv[2] if len(sys.argv) > 2 else "4:2,2:2,2:4,1:4,1:8,4:4").split(",")]
 s = torch.cuda.current_stream()
 L = wx.make_launch(stream=s.cuda_stream)
 Lt = wx.make_launch(stream=s.cuda_stream, flags=wx.F_TIME)
@@ -30,9 +31,10 @@ for n in sizes:
     t = wx.Table.from_tensors(price=price, quantity=key)
     res = {}
     for rnd in range(3):
-        for per_cu, unroll in cfgs:
+        for per_cu, unroll, gblock in cfgs:
             os.environ["WARPDB_GRID_PER_CU"] = per_cu
-            os.environ["WARPDB_EXTRA_DEFINES"] = "" if unroll == "2" else f"WX_UNROLL={unroll}"
+            os.environ["WARPDB_GBLOCK"] = gblock
+            os.environ["WARPDB_EXTRA_DEFINES"] = "" if unroll == "4" else f"WX_UNROLL={unroll}"
             for _ in range(3):
                 wx.group_sum(t, "price[idx]", "quantity[idx]", None, L, 0, cap, ok.data_ptr(), os_.data_ptr(),
                              oc.data_ptr(), d_n_groups=ng.data_ptr(), want_count=False)
@@ -45,11 +47,12 @@ for n in sizes:
             e1.record(s)
             torch.cuda.synchronize()
             kms, nl = wx.timing_read()
-            res.setdefault((per_cu, unroll), []).append((kms / nl * 1e3, e0.elapsed_time(e1) / 20 * 1e3))
+            res.setdefault((per_cu, unroll, gblock), []).append((kms / nl * 1e3, e0.elapsed_time(e1) / 20 * 1e3))
             assert int(ng.item()) == 1024
-    for (per_cu, unroll), v in res.items():
-        print(f"n={n:>11d} per_cu={per_cu} unroll={unroll}: kernel " +
+    for (per_cu, unroll, gblock), v in res.items():
+        print(f"n={n:>11d} gblock={gblock} per_cu={per_cu} unroll={unroll}: kernel " +
               " ".join(f"{a:.1f}" for a, _ in v) + " us | call " + " ".join(f"{b:.1f}" for _, b in v) + " us",
               flush=True)
     del price, key, t
 os.environ.pop("WARPDB_GRID_PER_CU")
+os.environ.pop("WARPDB_GBLOCK")

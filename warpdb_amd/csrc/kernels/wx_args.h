@@ -33,6 +33,9 @@ typedef unsigned int wx_u32;
 #define WX_COMPACT_DWAVES 15  // data waves per compaction workgroup (host passes its choice)
 #endif
 #define WX_GROUP_WINDOW 2048
+#ifndef WX_GBLOCK
+#define WX_GBLOCK 512  // wx_group_sum workgroup size (host and device agree through this header)
+#endif
 #define WX_GROUP_HSORT_MAX 4096
 #define WX_TOPK_MAX 32
 #define WX_TOPK_SLOTS 64        // top-K grid-wide bound: one slot per wave lane

@@ -197,8 +197,11 @@ __device__ __forceinline__ float ord2f(wx_u32 m) {
 #define WX_LOAD_U_FAST(name, T, slot) ::wx::load4_full<T>(wx_a.col[slot], wx_r0u, wx_u##slot[wx_u]);
 #define WX_LOAD_U(name, T, slot) ::wx::load4_tail<T>(wx_a.col[slot], wx_r0u, wx_a.n_rows, wx_u##slot[wx_u]);
 #define WX_BIND_U(name, T, slot) const ::wx::reg<T> name{wx_u##slot[wx_u][wx_e]};
-#define WX_SPAN ((wx_i64)WX_BLOCK * WX_UNROLL)
-#define WX_QUAD(u) (wx_base + (wx_i64)(u) * WX_BLOCK + threadIdx.x)
+// WX_LBLOCK: the block size of the kernel using the stride loop (WX_BLOCK
+// unless a kernel family redefines it around its kernel)
+#define WX_LBLOCK WX_BLOCK
+#define WX_SPAN ((wx_i64)WX_LBLOCK * WX_UNROLL)
+#define WX_QUAD(u) (wx_base + (wx_i64)(u) * WX_LBLOCK + threadIdx.x)
 // When the whole span lies inside the table (a workgroup-uniform test) the
 // loads are unconditional 16-byte loads; only the last span takes the
 // guarded path.
@@ -1359,10 +1362,11 @@ extern "C" __global__ __launch_bounds__(WX_SFIN_BLOCK) void wx_sum_finalize(WxSu
 // while every partial sum stays below 2^53 ulps of the smallest value.
 #define WX_GWIN WX_GROUP_WINDOW
 #ifndef WX_UNROLL
-// row quads per thread per span: 4 at 4 workgroups per CU, 1.158-1.169 vs
-// 1.177-1.182 ms per 1e9 rows for 2 (fewer workgroups per CU lose 6-85 %:
-// profiles/r03/abl_group_grid.txt)
-#define WX_UNROLL 4
+// row quads per thread per span, with WX_GBLOCK = 512 at 2 workgroups per
+// CU: 1.122-1.124 ms per 1e9 rows (148.6-149.5 us per 1.25e8) against
+// 1.155-1.157 (156-158 us) for 256-thread workgroups at 4 per CU with 4
+// quads and 1.177-1.182 with 2 (profiles/r03/abl_group_grid.txt)
+#define WX_UNROLL 2
 #endif
 #define WX_HSORT_MAX WX_GROUP_HSORT_MAX
 
@@ -1402,13 +1406,20 @@ __device__ __forceinline__ void wx_hash_add(const WxGroupArgs &a, int key, doubl
   atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_CAPACITY);
 }
 
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs wx_a) {
+// WX_GBLOCK threads per workgroup (wx_args.h; the host launches the same):
+// the window's global flush is one f64 + one u64 atomic per non-empty bin per
+// workgroup, 6-10 us per query at 4 x 256-thread workgroups per CU
+// (WX_DIAG_NO_FLUSH, profiles/r03/abl_group_flush.txt); fewer, larger
+// workgroups flush less for the same waves per CU.
+#undef WX_LBLOCK
+#define WX_LBLOCK WX_GBLOCK
+extern "C" __global__ __launch_bounds__(WX_GBLOCK) void wx_group_sum(WxGroupArgs wx_a) {
   __shared__ double wx_s_sum[WX_GWIN];
   __shared__ wx_u32 wx_s_cnt[WX_GWIN];
 #if WX_MINMAX
   __shared__ wx_u32 wx_s_min[WX_GWIN], wx_s_max[WX_GWIN];
 #endif
-  for (int i = threadIdx.x; i < WX_GWIN; i += WX_BLOCK) {
+  for (int i = threadIdx.x; i < WX_GWIN; i += WX_GBLOCK) {
     wx_s_sum[i] = 0.0;
     wx_s_cnt[i] = 0u;
 #if WX_MINMAX
@@ -1441,7 +1452,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_sum(WxGroupArgs 
 #ifndef WX_DIAG_NO_FLUSH
 #define WX_DIAG_NO_FLUSH 0  // diagnostic: the window's global flush skipped (results invalid)
 #endif
-  for (int i = threadIdx.x; i < WX_GWIN && !WX_DIAG_NO_FLUSH; i += WX_BLOCK) {
+  for (int i = threadIdx.x; i < WX_GWIN && !WX_DIAG_NO_FLUSH; i += WX_GBLOCK) {
     const wx_u32 c = wx_s_cnt[i];
     if (c) {
       atomicAdd(&wx_a.win_sum[i], wx_s_sum[i]);
@@ -2017,6 +2028,9 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_emit(WxG
     __syncthreads();
   }
 }
+
+#undef WX_LBLOCK
+#define WX_LBLOCK WX_BLOCK
 
 // One 1024-thread block: sort the general-key entries, merge with the dense
 // window in ascending key order, write the outputs, zero what was used.  The
