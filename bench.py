@@ -246,6 +246,7 @@ def pmc_traffic(workload, n, keys=1024):
 
 
 # ------------------------------------------------- result check
+SECONDARY_WARM_S = 0.1  # secondary lines: warm-up steps worth >= 0.1 s beyond --warmup (clock ramp, timed())
 CHECK_CHUNK = 1 << 28  # rows per torch pass of the check (bounds its temporaries)
 
 
@@ -277,9 +278,9 @@ def self_check(workload, sq, cols, n, world, wd, torch, out_v=None, keys=1024):
     _, expr, aux, _ = WORKLOADS[workload]
     mark = _mark
 
-    def red(x, op=torch.distributed.ReduceOp.SUM if world > 1 else None):
+    def red(x, op=torch.distributed.ReduceOp.SUM):
         t = torch.as_tensor(x, dtype=torch.float64, device="cuda").reshape(-1).clone()
-        return wd.all_reduce_(t, op=op) if world > 1 else t
+        return wd.all_reduce_(t, op=op)  # the identity without a process group
 
     def chunks():
         for c0 in range(0, n, CHECK_CHUNK):
@@ -389,7 +390,10 @@ def main_ranks(args):
     backend = os.environ.get("WARPDB_DIST_BACKEND", "nccl")
     local = local % max(1, torch.cuda.device_count()) if backend == "gloo" else local
     torch.cuda.set_device(local)
-    if world > 1:
+    # WARPDB_EXCHANGE_ONE_RANK=1 (test hook): the exchanges run with one rank
+    # too, so a one-GPU box runs the RCCL collectives of the multi-rank step
+    coll = world > 1 or wd.exchange_one_rank()
+    if coll:
         if backend == "gloo":
             dist.init_process_group("gloo")
         else:
@@ -449,7 +453,7 @@ def main_ranks(args):
             sq.sum_device(expr, aux, res)
     elif workload == "group":
         def step():
-            if world > 1 and args.keys > wx.GROUP_WINDOW_BINS:
+            if coll and args.keys > wx.GROUP_WINDOW_BINS:
                 # keys beyond the window may outgrow the exchange slots: the
                 # host-checked form, which takes the variable-size merge then
                 sq.group_sum(expr, aux, None, 0, group_capacity(args.keys))
@@ -465,28 +469,45 @@ def main_ranks(args):
         if verbose:
             print(f"[bench rank {rank}] {what} {time.strftime('%H:%M:%S')}", file=sys.stderr, flush=True)
 
-    def timed(step_fn):
-        """W warm-up steps, then exactly K steps between barrier + synchronize;
+    def timed(step_fn, warm_s=0.0):
+        """W warm-up steps (secondary lines: and at least warm_s seconds of
+        them), then exactly K steps between barrier + synchronize;
         (elapsed s, average timed-kernel ms, launches), max over ranks."""
         for _ in range(args.warmup):
             step_fn()
+        if warm_s > 0:
+            # after any host-side pause (the previous line's check) the first
+            # ~20 ms of launches run slower while the clocks ramp back up
+            # (profiles/r03/thermal_group.txt: 1.18 vs 1.13 ms per GROUP BY)
+            # the same number of extra steps on every rank (each step may hold a collective)
+            torch.cuda.synchronize()
+            w0 = time.perf_counter()
+            step_fn()
+            torch.cuda.synchronize()
+            extra = min(2000, int(warm_s / max(1e-5, time.perf_counter() - w0)) + 1)
+            if coll:
+                t = torch.tensor([float(extra)], dtype=torch.float64, device="cuda")
+                wd.all_reduce_(t, op=dist.ReduceOp.MAX)
+                extra = int(t[0])
+            for _ in range(extra):
+                step_fn()
         wx.check(L)
         wx.timing_read()  # discard the warm-up launches
         mark("timed steps")
-        if world > 1:
+        if coll:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step_fn()
         torch.cuda.synchronize()
-        if world > 1:
+        if coll:
             dist.barrier()
         el = time.perf_counter() - t0
         k_ms, nl = wx.timing_read()
         wx.check(L)
         k_avg = k_ms / max(1, nl)
-        if world > 1:
+        if coll:
             t = torch.tensor([el, k_avg], dtype=torch.float64, device="cuda")
             wd.all_reduce_(t, op=dist.ReduceOp.MAX)
             el, k_avg = float(t[0]), float(t[1])
@@ -529,7 +550,7 @@ def main_ranks(args):
                                        "group": f"one all-reduce of {wd_group_doubles(world)} x f64 (key window + "
                                                 f"{world} slots of out-of-window groups), wx_group_combine_slots",
                                        "topk": "all-gather 520 B per shard, wx_topk_merge",
-                                       "dense": "none", "sort": "none"}[workload] if world > 1 else "none (1 GPU)",
+                                       "dense": "none", "sort": "none"}[workload] if coll else "none (1 GPU)",
                           "parallelism": f"row-sharded x{world}, one process per GPU"}
         if passing is not None:
             line["config"]["passing_rows_per_gpu"] = passing
@@ -561,7 +582,7 @@ def main_ranks(args):
                 def step2():
                     sq2.group_sum_device(e2, a2, None, 0, group_capacity(1024))
             mark(f"secondary {w2}")
-            el2, k2_ms, _ = timed(step2)
+            el2, k2_ms, _ = timed(step2, SECONDARY_WARM_S)
             chk2 = None if args.no_check else self_check(w2, sq2, cols2, n, world, wd, torch)
             b2 = n * READ_BYTES[w2]
             secondary[w2] = {"query": WORKLOADS[w2][0], "value": round(n_total * args.steps / el2, 1),
@@ -589,7 +610,7 @@ def main_ranks(args):
             def step3():
                 sq3.group_sum_device(e3x, a3x, None, 0, group_capacity(1024))
             mark("secondary c3")
-            el3, k3_ms, _ = timed(step3)
+            el3, k3_ms, _ = timed(step3, SECONDARY_WARM_S)
             chk3 = None if args.no_check else self_check("group", sq3, cols3, n3, world, wd, torch)
             secondary["c3_group_strong"] = {
                 "query": WORKLOADS["group"][0], "config": f"C3: {c3_total:.3g} rows over all GPUs (strong scaling)",
@@ -614,7 +635,7 @@ def main_ranks(args):
             def step4():
                 sq4.sum_device(e4x, a4x, res4)
             mark("secondary c4")
-            el4, k4_ms, _ = timed(step4)
+            el4, k4_ms, _ = timed(step4, SECONDARY_WARM_S)
             chk4 = None if args.no_check else self_check("sum", sq4, {"price": p4}, n4, world, wd, torch)
             secondary["c4_sum_strong"] = {
                 "query": WORKLOADS["sum"][0], "config": f"C4: {c4_total:.3g} rows over all GPUs (strong scaling)",
@@ -628,7 +649,7 @@ def main_ranks(args):
             line["secondary"] = secondary
         line["cpu_baseline"] = cpu_leg(args, workload) if world == 1 else None
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if coll:
         dist.destroy_process_group()
 
 
@@ -675,9 +696,13 @@ def main_api(args):
     line = line_common(args, shards.num_shards, n_total, elapsed, workload)
     line["config"] = {"workload": f"{query} ({workload})", "rows_per_gpu": n_max, "total_rows": n_total,
                       "api": "pywarpdb.ResidentShards (WarpDB::query_multi_gpu_sum / _group / _topk)",
-                      "exchange": {"sum": "ncclAllReduce 2 x f64", "group": "ncclAllReduce 4097 x f64",
-                                   "topk": "ncclAllGather 520 B per shard"}[workload] +
-                                  " over ncclCommInitAll(devices 0..n-1)",
+                      "exchange": ({"sum": "ncclAllReduce 2 x f64",
+                                    "group": f"ncclAllReduce {api_group_doubles(shards.num_shards)} x f64 (key window + "
+                                             f"per-shard slots), wx_group_combine_slots",
+                                    "topk": "ncclAllGather 520 B per shard, wx_topk_merge"}[workload] +
+                                   " over ncclCommInitAll(devices 0..n-1)")
+                                  if shards.num_shards > 1 or os.environ.get("WARPDB_EXCHANGE_ONE_RANK") == "1"
+                                  else "none (1 GPU)",
                       "parallelism": f"row-sharded x{shards.num_shards}, one process, one thread + stream per GPU"}
     # the C++ path has no per-kernel events: the whole step bounds the kernel
     ms = elapsed / args.steps * 1e3
@@ -687,6 +712,14 @@ def main_api(args):
     line["check"] = api_check(workload, step(), n_total)
     line["cpu_baseline"] = cpu_leg(args, workload) if shards.num_shards == 1 else None
     print(json.dumps(line), flush=True)
+
+
+def api_group_doubles(shards):
+    """ResidentShards::group_sum's exchange buffer (multi_gpu.cpp: 64 groups
+    per slot, at most 4096 slot groups in all)."""
+    from warpdb_amd import _warpexec as wx
+
+    return wx.group_slots_doubles(shards, max(1, min(64, 4096 // shards)))
 
 
 def api_check(workload, res, n_total):

@@ -10,6 +10,10 @@
   heavy ties, NaN, +/-0.0, fewer rows than K, both directions, K = 1..32.
 * The multi-rank bench under torchrun with RCCL (the default backend) when
   more than one GPU is visible -- skipped on a one-GPU box.
+* The same multi-rank step, ResidentShards and WarpDB::query_multi_gpu_*
+  with a ONE-rank communicator (WARPDB_EXCHANGE_ONE_RANK=1): on a one-GPU
+  box this executes the RCCL all-reduce / all-gather calls and the buffers
+  they hand to the exchange kernels.
 """
 from __future__ import annotations
 
@@ -228,11 +232,15 @@ def test_bench_rccl_ranks(workload, extra):
     """bench.py under torchrun with the default (RCCL) backend, one rank per
     visible GPU (at most 8): the product's exchanges over xGMI, each line's
     own result check."""
-    n = min(8, _ngpus())
+    _bench_ranks(min(8, _ngpus()), workload, extra)
+
+
+def _bench_ranks(n, workload, extra, env_extra=None):
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
         port = s.getsockname()[1]
     env = {k: v for k, v in os.environ.items() if k != "WARPDB_DIST_BACKEND"}
+    env.update(env_extra or {})
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(n),
                         "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.join(ROOT, "bench.py"),
                         "--gpus", str(n), "--workload", workload, "--steps", "3", "--warmup", "1",
@@ -243,12 +251,54 @@ def test_bench_rccl_ranks(workload, extra):
     assert d["n_gpus"] == n and d["value"] > 0 and str(d["check"]).startswith("ok"), d
     for v in (d.get("secondary") or {}).values():
         assert str(v["check"]).startswith("ok"), v
+    return d
+
+
+@pytest.mark.parametrize("workload,extra", [
+    ("project", ["--rows", "1e7", "--c4-rows", "20000001", "--c3-rows", "10000001"]),
+    ("sum", ["--total-rows", "20000001"]),
+    ("group", ["--rows", "1e7"]),
+    ("group", ["--rows", "3e6", "--keys", "3000"]),  # keys beyond the window: slots, then the -2 merge
+    ("topk", ["--rows", "1e7"]),
+])
+def test_bench_rccl_one_rank(workload, extra):
+    """The multi-rank step of bench.py on a one-rank RCCL communicator
+    (WARPDB_EXCHANGE_ONE_RANK=1, default backend): torch.distributed's
+    all_reduce / all_gather_into_tensor on RCCL with the exchange buffers the
+    8-GPU run hands over (counts, {sum, count}, window + slots, top-K
+    records), the exchange kernels behind them, every line self-checked."""
+    d = _bench_ranks(1, workload, extra, {"WARPDB_EXCHANGE_ONE_RANK": "1"})
+    assert d["config"]["exchange"] != "none (1 GPU)", d["config"]
+
+
+@pytest.mark.parametrize("workload", ["sum", "group", "topk"])
+def test_bench_api_rccl_one_device(workload):
+    """ResidentShards (the C++ multi-GPU path) with a one-device
+    ncclCommInitAll communicator: ncclAllReduce / ncclAllGather run."""
+    env = dict(os.environ, WARPDB_EXCHANGE_ONE_RANK="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--api", "--gpus", "1", "--workload", workload,
+                        "--rows", "1e7", "--steps", "3", "--warmup", "1", "--no-cpu-baseline"],
+                       capture_output=True, text=True, cwd=ROOT, env=env, timeout=300)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
+    d = [json.loads(x) for x in r.stdout.splitlines() if x.startswith("{")][-1]
+    assert str(d["check"]).startswith("ok") and "nccl" in d["config"]["exchange"], d
 
 
 @pytest.mark.skipif(torch.cuda.device_count() < 2, reason="one GPU visible: the RCCL runs need a multi-GPU box")
 def test_warpdb_multi_gpu_all_devices_against_oracle(tmp_path):
     """WarpDB::query_multi_gpu{,_sum,_group,_topk} over every visible GPU
     (ncclCommInitAll, one thread + stream per device) against the oracle."""
+    _warpdb_multi_against_oracle(tmp_path)
+
+
+def test_warpdb_multi_gpu_one_device_rccl_against_oracle(tmp_path, monkeypatch):
+    """The same on one device with its exchanges on a one-device RCCL
+    communicator (WARPDB_EXCHANGE_ONE_RANK=1)."""
+    monkeypatch.setenv("WARPDB_EXCHANGE_ONE_RANK", "1")
+    _warpdb_multi_against_oracle(tmp_path)
+
+
+def _warpdb_multi_against_oracle(tmp_path):
     from warpdb_amd import pywarpdb as pw
 
     m = 200_003

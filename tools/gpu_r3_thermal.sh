@@ -4,5 +4,5 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
 O=$R/gpurun_out/r3th
 mkdir -p "$O"
-timeout -k 10 300 python3 tools/thermal_group.py > "$O/thermal_group.txt" 2>&1
+timeout -k 10 300 python3 tools/thermal_group.py > "$O/thermal_group2.txt" 2>&1
 echo done

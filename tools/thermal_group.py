@@ -61,3 +61,15 @@ time.sleep(10)
 print(f"after 10 s idle: group {group_ms():.4f} ms", flush=True)
 project(20)
 print(f"after 20 s of compaction: group {group_ms():.4f} ms", flush=True)
+# how fast the clocks come back: 20-launch windows (~23 ms each) after idle gaps
+for gap in (0.2, 1.0, 3.0, 10.0):
+    project(3)
+    time.sleep(gap)
+    print(f"after {gap} s idle, consecutive 20-launch windows: " +
+          " ".join(f"{group_ms():.4f}" for _ in range(12)), flush=True)
+# the same after a busy-wait on the host with the GPU idle (what a host-side self-check looks like)
+project(3)
+t0 = time.time()
+while time.time() - t0 < 1.0:
+    pass
+print("after 1 s host busy: " + " ".join(f"{group_ms():.4f}" for _ in range(12)), flush=True)

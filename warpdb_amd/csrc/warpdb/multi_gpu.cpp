@@ -51,6 +51,14 @@ int virtual_shards() {
   return v ? std::max(0, std::atoi(v)) : 0;
 }
 
+// Test hook: WARPDB_EXCHANGE_ONE_RANK=1 runs the RCCL exchanges even for a
+// single shard (a one-device communicator), so a one-GPU box executes the
+// ncclAllReduce / ncclAllGather calls and the buffers they hand over.
+bool exchange_one_rank() {
+  const char *v = std::getenv("WARPDB_EXCHANGE_ONE_RANK");
+  return v && v[0] == '1' && v[1] == 0;
+}
+
 // shards to plan when the caller asks for every device
 int shard_count() {
   const int v = virtual_shards();
@@ -216,7 +224,7 @@ namespace {
 void allreduce_f64(const std::vector<ShardRange> &shards, const std::vector<double *> &bufs,
                    const std::vector<hipStream_t> &streams, size_t count) {
   const int nshard = static_cast<int>(shards.size());
-  if (nshard < 2) return;
+  if (nshard < 1 || (nshard < 2 && !exchange_one_rank())) return;
   if (!distinct_devices(shards)) {  // co-located shards (WARPDB_VIRTUAL_SHARDS): sum through the host
     std::vector<double> acc(count, 0.0), part(count);
     for (int i = 0; i < nshard; ++i) {
@@ -462,6 +470,7 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
                      reinterpret_cast<int64_t *>(c + kTopkMax * 16), nullptr, err, sizeof(err)),
              err);
   });
+  bool gathered = ns > 1;  // the records of every shard are in each shard's `all`
   if (ns > 1 && !distinct_devices(ranges)) {  // co-located shards (WARPDB_VIRTUAL_SHARDS): gather through the host
     std::vector<char> all(kTopkRec * ns);
     for (size_t i = 0; i < ns; ++i) {
@@ -474,7 +483,8 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
       DevGuard g(ranges[i].device);
       hip_ok(hipMemcpy(impl_->topk[i].all.ptr, all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy");
     }
-  } else if (ns > 1) {
+  } else if (ns > 1 || exchange_one_rank()) {
+    gathered = true;
     Comms &cm = comms_for(static_cast<int>(ns));
     std::lock_guard<std::mutex> clk(cm.mu);
     if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
@@ -500,7 +510,7 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
     DevGuard dg(dev0);
     wx_launch L = sync_launch(dev0, streams[0]);
     L.flags = 0;
-    throw_on(wx_topk_merge(static_cast<const wx_topk_record *>(ns > 1 ? t0.all.ptr : t0.cand.ptr),
+    throw_on(wx_topk_merge(static_cast<const wx_topk_record *>(gathered ? t0.all.ptr : t0.cand.ptr),
                            static_cast<int32_t>(ns), k, descending ? 1 : 0, &L, reinterpret_cast<float *>(o),
                            reinterpret_cast<int64_t *>(o + kTopkMax * 8), reinterpret_cast<float *>(o + kTopkMax * 4),
                            reinterpret_cast<int64_t *>(o + kTopkMax * 16), nullptr, err, sizeof(err)),

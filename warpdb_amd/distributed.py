@@ -28,9 +28,14 @@ With the "nccl" backend these run on RCCL over xGMI on device tensors; with
 through host tensors.  Without an initialised process group (one GPU, one
 process) every exchange is the identity.  bench.py times exactly these
 functions.
+
+Test hook: WARPDB_EXCHANGE_ONE_RANK=1 runs the multi-rank exchanges even
+with one rank, so a one-GPU box executes the RCCL collectives (a one-rank
+communicator) and the exchange kernels end to end.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import List, Optional, Tuple
 
@@ -48,8 +53,16 @@ def shard_range(n_rows: int, world: int, rank: int) -> Tuple[int, int]:
     return b, min(n_rows, b + chunk)
 
 
+def exchange_one_rank() -> bool:
+    """Test hook: the exchanges run even with one rank (WARPDB_EXCHANGE_ONE_RANK=1)."""
+    return os.environ.get("WARPDB_EXCHANGE_ONE_RANK") == "1"
+
+
 def _single(group=None) -> bool:
-    return not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1
+    """True when there is nothing to exchange (no process group, or one rank)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return True
+    return dist.get_world_size(group) == 1 and not exchange_one_rank()
 
 
 def _world(group=None) -> int:
@@ -252,6 +265,7 @@ class ShardedQuery:
         self.group = group
         self.table = shard.table()
         self.world = _world(group)
+        self.exchange = not _single(group)  # the multi-rank exchanges run
         dev = torch.cuda.current_device()
         stream = torch.cuda.current_stream().cuda_stream
         self.launch = wx.make_launch(device=dev, stream=stream, custom_src=custom_src, flags=flags)
@@ -327,7 +341,7 @@ class ShardedQuery:
         shard's general-key table overflowed.  One shard: wx_group_sum alone."""
         wx = self.wx
         S, ex, xk, xs, xc, nx, ok, osm, oc, ng = self._group_bufs(capacity)
-        if self.world == 1:  # one shard: the single-GPU kernel + finalize, nothing to exchange or read back
+        if not self.exchange:  # one shard: the single-GPU kernel + finalize, nothing to exchange or read back
             wx.group_sum(self.table, val_expr, key_expr, cond, self.launch, key_lo, capacity, ok.data_ptr(),
                          osm.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr(), want_count=False)
             return ok, osm, oc, ng
@@ -348,7 +362,7 @@ class ShardedQuery:
         wx = self.wx
         ok, osm, oc, ng = self.group_sum_device(val_expr, key_expr, cond, key_lo, capacity)
         n = int(ng.item())  # synchronises
-        if self.world > 1:
+        if self.exchange:
             S, ex, xk, xs, xc, nx = self._group_bufs(capacity)[:6]
             counts = group_slot_counts(ex.cpu(), self.world, S)
             err = group_exchange_error(counts, capacity)
@@ -389,7 +403,7 @@ class ShardedQuery:
         """Global top-K left in HBM, no host synchronisation: this shard's
         record, one all-gather, wx_topk_merge.  Returns (keys, rows, vals, count)."""
         rec = self.topk_device(order_expr, cond, select_expr, k, descending)
-        if self.world == 1:  # one shard's list is final (its count is already <= k)
+        if not self.exchange:  # one shard's list is final (its count is already <= k)
             rk, rv, ri, rn = topk_record_views(rec)
             return rk[:k], ri[:k], rv[:k], rn
         return merge_topk_device(rec, k, descending, self.launch_aux, self._buf("tmk", k, torch.float32),
