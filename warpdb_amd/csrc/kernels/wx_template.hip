@@ -3222,6 +3222,23 @@ __device__ __forceinline__ void wx_rs_load(const WxRadixPassArgs &a, wx_i64 wb, 
   }
 }
 
+#ifndef WX_RS_FOLD_LD
+// the digit's tile-local base folded into the per-wave counts once per tile
+// (2 048 adds), so the permutation reads one LDS word per key, not two
+#define WX_RS_FOLD_LD 1
+#endif
+#ifndef WX_RS_RANK_ATOMIC
+// Rank by one returning LDS add per key (ds_add_rtn_u32 on the wave's digit
+// counter): the LDS serialises the lanes of one instruction that hit the
+// same counter in ascending lane order, so the returned counts are the
+// stable in-wave ranks; the adds of item i + 1 follow item i's (one wave's
+// LDS operations execute in order), so all items' adds issue back to back
+// with one wait.  Lane 0's digit group (a few-valued digit -- the exponent
+// byte -- sends most of a wave to one counter) adds its size once from lane
+// 0 and ranks by its ballot.  0 selects the peer-mask form below.
+#define WX_RS_RANK_ATOMIC 0
+#endif
+
 // In-wave stable rank of each key among the wave's keys with the same digit:
 // the group's lowest lane bumps the wave's count and broadcasts the old one.
 template <int KIND, bool ASC>
@@ -3229,6 +3246,28 @@ __device__ __forceinline__ void wx_rs_rank(const WxRadixPassArgs &a, WxRsShared 
                                            const wx_u32 (&x)[WX_RS_ITEMS], wx_u32 (&rk)[WX_RS_ITEMS]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const wx_u64 below = (1ull << lane) - 1ull;
+#if WX_RS_RANK_ATOMIC
+  (void)peers;
+  wx_u32 lead_bits = 0u;  // bit i: this lane is in lane 0's digit group of item i (and not lane 0)
+#pragma unroll
+  for (int i = 0; i < WX_RS_ITEMS; ++i) {
+    const bool valid = wb + (wx_i64)i * 64 < a.n;
+    const wx_u32 d = (wx_rs_key_t<KIND, ASC>(x[i]) >> a.shift) & 255u;
+    const wx_u32 d0 = __builtin_amdgcn_readfirstlane(d);
+    const bool lead = valid && d == d0;
+    const wx_u64 lm = __builtin_amdgcn_ballot_w64(lead);
+    rk[i] = (wx_u32)__builtin_popcountll(lm & below);
+    if (valid && (!lead || lane == 0))
+      rk[i] = atomicAdd(&S.wc[wave][d], lead ? (wx_u32)__builtin_popcountll(lm) : 1u);
+    lead_bits |= (lead && lane != 0 ? 1u : 0u) << i;
+  }
+#pragma unroll
+  for (int i = 0; i < WX_RS_ITEMS; ++i) {
+    const wx_u32 base0 = __builtin_amdgcn_readlane(rk[i], 0);  // lane 0's returned count
+    if ((lead_bits >> i) & 1u) rk[i] += base0;
+  }
+  return;
+#endif
   constexpr int G = WX_RS_RANK_G;
 #pragma unroll
   for (int i = 0; i < WX_RS_ITEMS; i += G) {
@@ -3383,6 +3422,10 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
   if (tid < 256) {
     wx_u32 ld = inc - tot;
     for (int w = 0; w < wave; ++w) ld += S.wsum[w];
+    if (WX_RS_FOLD_LD) {
+#pragma unroll
+      for (int w = 0; w < WX_RS_WAVES; ++w) S.wc[w][tid] += ld;  // the scatter's slot base in one word
+    }
     wx_u64 excl = 0;
     if (look) {
       // WX_RS_LBW predecessors per round, loads in flight together; stop at
@@ -3622,6 +3665,10 @@ __device__ __forceinline__ void wx_rs_digits_pair(const WxRadixPassArgs &a, WxRs
     const wx_u32 tot = S.tt[d];
     wx_u32 ld = S.inc[d] - tot;
     for (int w = 0; w < (d >> 6); ++w) ld += S.wsum[w];
+    if (WX_RS_FOLD_LD) {
+#pragma unroll
+      for (int w = 0; w < WX_RS_WAVES; ++w) S.wc[w][d] += ld;
+    }
     if (look) wx::st_agent(&a.status[(wx_u64)tile * 256 + d], E | WX_RS_FLAG_P | (excl + tot));
     S.gb[d] = a.digit_base[d] + (wx_u32)excl - ld;
     S.ld[d] = ld;
@@ -3667,6 +3714,10 @@ __device__ __forceinline__ wx_u32 wx_rs_local(const WxRadixPassArgs &a, WxRsShar
     wx_u32 ld = inc - tot;
     for (int w = 0; w < wave; ++w) ld += S.wsum[w];
     S.ld[tid] = ld;
+    if (WX_RS_FOLD_LD) {
+#pragma unroll
+      for (int w = 0; w < WX_RS_WAVES; ++w) S.wc[w][tid] += ld;
+    }
   }
   return tot;
 }
@@ -3744,7 +3795,7 @@ __device__ __forceinline__ void wx_rs_scatter(const WxRadixPassArgs &a, WxRsShar
     wx_u32 p = 0u;
     if (wb + (wx_i64)i * 64 < a.n) {
       const wx_u32 d = (wx_rs_key_t<KIND, ASC>(x[i]) >> a.shift) & 255u;
-      p = S.ld[d] + S.wc[wave][d] + rk[i];
+      p = (WX_RS_FOLD_LD ? 0u : S.ld[d]) + S.wc[wave][d] + rk[i];
       if (WX_RS_DIAG_NO_RANK) p = (wx_u32)(wave * 64 * WX_RS_ITEMS + i * 64 + (threadIdx.x & 63));
       s_k[p] = x[i];
     }
@@ -3808,7 +3859,7 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
   if (tid == 0) S.tk[0] = atomicAdd(&a.ctl[0], 1u);
   wx_u64 *peers = reinterpret_cast<wx_u64 *>(s_k);
   for (int i = tid; i < WX_RS_WAVES * 256; i += WX_RS_BLOCK) (&S.wc[0][0])[i] = 0u;
-  if (WX_RS_MATCH_LDS)
+  if (WX_RS_MATCH_LDS && !WX_RS_RANK_ATOMIC)
     for (int i = tid; i < WX_RS_RANK_G * WX_RS_WAVES * 256; i += WX_RS_BLOCK) peers[i] = 0ull;
   __syncthreads();
   const wx_u32 tile = S.tk[0];
