@@ -336,7 +336,10 @@ def self_check(workload, sq, cols, n, world, wd, torch, out_v=None, keys=1024):
             raise SystemExit(f"check failed: SUM {got_s} / {got_c} vs {float(want[0])} / {int(want[1])}")
         return f"ok: count {got_c} exact, sum {got_s:.6e} within 1e-12"
     if workload == "group":
-        gk, gs, gc = sq.group_sum(expr, aux, None, 0, group_capacity(keys))
+        if keys > wx.GROUP_WINDOW_BINS:  # the timed many-key form: list records + wx_group_merge_lists
+            gk, gs, gc = sq.group_sum_lists(expr, aux, None, group_capacity(keys))
+        else:
+            gk, gs, gc = sq.group_sum(expr, aux, None, 0, group_capacity(keys))
         key = cols["quantity"]
         ws = torch.zeros(keys, dtype=torch.float64, device="cuda")
         wc = torch.zeros(keys, dtype=torch.float64, device="cuda")
@@ -454,9 +457,9 @@ def main_ranks(args):
     elif workload == "group":
         def step():
             if coll and args.keys > wx.GROUP_WINDOW_BINS:
-                # keys beyond the window may outgrow the exchange slots: the
-                # host-checked form, which takes the variable-size merge then
-                sq.group_sum(expr, aux, None, 0, group_capacity(args.keys))
+                # many keys: every shard's groups as one list record, ONE
+                # all-gather, wx_group_merge_lists on the device
+                sq.group_sum_lists_device(expr, aux, None, group_capacity(args.keys))
             else:
                 sq.group_sum_device(expr, aux, None, 0, group_capacity(args.keys))
     else:

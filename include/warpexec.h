@@ -233,6 +233,32 @@ wx_status wx_group_combine_slots(const double *d_exchange, int32_t n_slots, int3
                                  int32_t *d_keys, double *d_sums, int64_t *d_counts, int64_t *d_n_groups,
                                  int64_t *h_n_groups, char *err, size_t errlen);
 
+/* Row-sharded GROUP BY with many groups per shard, in ONE collective and no
+ * host read (replaces the host-side gather and merge of shard results,
+ * src/multi_gpu_utils.cpp:23-60 / src/warpdb.cpp:508-542, for results that
+ * outgrow the exchange slots).  Each shard writes its groups -- keys
+ * ascending and unique, e.g. straight from wx_group_sum, or the out-of-window
+ * groups of wx_group_partials_slots -- into one fixed-size list record of
+ * WX_GROUP_LIST_BYTES(list_capacity) bytes: int64 count at offset 0, then
+ * list_capacity int32 keys, doubles sums at WX_GROUP_LIST_SUMS_OFF, int64
+ * counts at WX_GROUP_LIST_COUNTS_OFF.  One all-gather of the records
+ * (ncclAllGather, bytes) hands every rank the n_lists records back to back;
+ * this call merges them on the device: groups of equal key summed in list
+ * order (so every rank computes the same bits), then, with d_window (the
+ * combined wx_group_partials window, nullable), merged with the window's
+ * non-empty bins, none of whose keys may appear in a list.  Ascending keys,
+ * at most `capacity` written; the count goes to d_n_groups / h_n_groups.
+ * It is -1 when a list's count is negative or above list_capacity (a shard
+ * whose table or list overflowed): every rank sees the same records, so
+ * every rank gets the same -1.  1 <= n_lists <= 1024. */
+#define WX_GROUP_LIST_SUMS_OFF(cap) (8 + 8 * (((int64_t)(cap) + 1) / 2))
+#define WX_GROUP_LIST_COUNTS_OFF(cap) (WX_GROUP_LIST_SUMS_OFF(cap) + 8 * (int64_t)(cap))
+#define WX_GROUP_LIST_BYTES(cap) (WX_GROUP_LIST_COUNTS_OFF(cap) + 8 * (int64_t)(cap))
+wx_status wx_group_merge_lists(const void *d_lists, int32_t n_lists, int64_t list_capacity,
+                               const double *d_window, int32_t key_window_lo, const wx_launch *launch,
+                               int64_t capacity, int32_t *d_keys, double *d_sums, int64_t *d_counts,
+                               int64_t *d_n_groups, int64_t *h_n_groups, char *err, size_t errlen);
+
 /* dst[i] = (dst type) src[i] for i < n, types in wx_dtype numbering (not
  * WX_STRING); C conversion semantics. */
 wx_status wx_cast(const void *d_src, int32_t src_dtype, void *d_dst, int32_t dst_dtype, int64_t n,

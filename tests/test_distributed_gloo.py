@@ -86,6 +86,47 @@ def group_combine_slots_emulated(ex, world, slot_groups, key_lo):
                                   np.array([acc[k][0] for k in ks]), np.array([acc[k][1] for k in ks], np.int64))
 
 
+def group_list_record(keys, sums, counts, cap, count=None):
+    """One shard's group list record (wx_group_merge_lists layout) as bytes:
+    int64 count | int32 keys[cap] padded to 8 B | f64 sums[cap] | int64 counts[cap]."""
+    from warpdb_amd import _warpexec as wx
+
+    nbytes, so, co = wx.group_list_layout(cap)
+    rec = np.zeros(nbytes, np.uint8)
+    m = len(keys)
+    rec[0:8] = np.array([m if count is None else count], np.int64).view(np.uint8)
+    rec[8:8 + 4 * m] = np.asarray(keys, np.int32).view(np.uint8)
+    rec[so:so + 8 * m] = np.asarray(sums, np.float64).view(np.uint8)
+    rec[co:co + 8 * m] = np.asarray(counts, np.int64).view(np.uint8)
+    return rec
+
+
+def group_merge_lists_emulated(allr, n_lists, cap, window, key_lo):
+    """wx_group_merge_lists' contract: -1 on a bad list count, else equal keys
+    summed in list order, merged with the window's non-empty bins."""
+    from warpdb_amd import _warpexec as wx
+
+    nbytes, so, co = wx.group_list_layout(cap)
+    recs = allr.reshape(n_lists, nbytes)
+    acc = {}
+    for rec in recs:
+        m = int(rec[0:8].view(np.int64)[0])
+        if m < 0 or m > cap:
+            return -1
+        ks, ss, cs = rec[8:8 + 4 * m].view(np.int32), rec[so:so + 8 * m].view(np.float64), rec[co:co + 8 * m].view(
+            np.int64)
+        for j in range(m):
+            a = acc.setdefault(int(ks[j]), [None, 0])
+            a[0] = ss[j] if a[0] is None else a[0] + ss[j]
+            a[1] += int(cs[j])
+    kk = sorted(acc)
+    xk, xs, xc = (np.array(kk, np.int32), np.array([acc[k][0] for k in kk], np.float64),
+                  np.array([acc[k][1] for k in kk], np.int64))
+    if window is None:
+        return xk, xs, xc
+    return group_combine_emulated(window, key_lo, xk, xs, xc)
+
+
 def topk_record(keys, vals, rows):
     """One wx_topk_record (include/warpexec.h) as bytes: unused slots junk."""
     rec = np.zeros(520, np.uint8)
@@ -152,10 +193,14 @@ def _worker(rank: int, world: int, port: int, n: int, errq):
         # window all-reduce + merge of the out-of-window groups only).  With
         # key_lo = 512 half of the 1024 keys fall outside the window.
         k, sm, cn = ora.group_sum(loc3, "price", "quantity")
-        gk, gsum, gcnt = wd.merge_groups(torch.from_numpy(k), torch.from_numpy(sm), torch.from_numpy(cn), len(k))
+        # every shard's whole group list, ONE all-gather of the fixed-size
+        # records, the wx_group_merge_lists contract (no window)
+        CAP = 1100
+        allr = wd.all_gather(torch.from_numpy(group_list_record(k, sm, cn, CAP)))
+        gk, gsum, gcnt = group_merge_lists_emulated(allr.numpy(), world, CAP, None, 0)
         rk, rsum, rcnt = ora.group_sum(ora.HostTable(full3), "price", "quantity")
-        assert np.array_equal(gk.numpy(), rk) and np.array_equal(gcnt.numpy(), rcnt)
-        assert np.array_equal(gsum.numpy(), rsum)  # exact: float values summed in double
+        assert np.array_equal(gk, rk) and np.array_equal(gcnt, rcnt)
+        assert np.allclose(gsum, rsum, rtol=1e-12, atol=0)
         for key_lo in (0, 512, -5000):
             win, xk, xs, xc = group_partials_emulated(k, sm, cn, key_lo)
             wt = torch.from_numpy(win)
@@ -165,10 +210,11 @@ def _worker(rank: int, world: int, port: int, n: int, errq):
             assert (n_extra_total > 0) == (outside > 0) and n_extra_total >= outside  # shards' counts, summed
             mk = np.zeros(0, np.int32); ms = np.zeros(0); mc = np.zeros(0, np.int64)
             if n_extra_total:
-                a, b_, c_ = wd.merge_groups(torch.from_numpy(xk), torch.from_numpy(xs), torch.from_numpy(xc), len(xk))
-                mk, ms, mc = a.numpy(), b_.numpy(), c_.numpy()
+                allr = wd.all_gather(torch.from_numpy(group_list_record(xk, xs, xc, CAP)))
+                mk, ms, mc = group_merge_lists_emulated(allr.numpy(), world, CAP, None, 0)
             ck, cs, cc = group_combine_emulated(wt.numpy(), key_lo, mk, ms, mc)
-            assert np.array_equal(ck, rk) and np.array_equal(cc, rcnt) and np.array_equal(cs, rsum), key_lo
+            assert np.array_equal(ck, rk) and np.array_equal(cc, rcnt), key_lo
+            assert np.allclose(cs, rsum, rtol=1e-12, atol=0), key_lo
 
         # SUM through the product's one-collective layout {sum, count as f64}
         out = torch.tensor([s, float(c)], dtype=torch.float64)
@@ -186,11 +232,10 @@ def _worker(rank: int, world: int, port: int, n: int, errq):
                 counts = wd.group_slot_counts(ex, world, S)
                 assert wd.group_exchange_error(counts, 1 << 16) is None
                 res = group_combine_slots_emulated(ex.numpy(), world, S, key_lo)
-                if res == -2:  # the fallback: variable-size merge, then the plain combine
+                if res == -2:  # the fallback: every shard's whole list record, one all-gather, the list merge
                     assert max(counts) > S
-                    a, b_, c_ = wd.merge_groups(torch.from_numpy(xk), torch.from_numpy(xs), torch.from_numpy(xc),
-                                                counts[rank])
-                    res = group_combine_emulated(ex.numpy()[:2 * 2048 + 1], key_lo, a.numpy(), b_.numpy(), c_.numpy())
+                    allr = wd.all_gather(torch.from_numpy(group_list_record(xk, xs, xc, CAP)))
+                    res = group_merge_lists_emulated(allr.numpy(), world, CAP, ex.numpy()[:2 * 2048 + 1], key_lo)
                 else:
                     assert max(counts) <= S
                 ck, cs, cc = res
@@ -204,6 +249,9 @@ def _worker(rank: int, world: int, port: int, n: int, errq):
         wd.all_reduce_(ex)
         errs = wd.group_exchange_error(wd.group_slot_counts(ex, world, 64), 1 << 16)
         assert errs is not None and "shard 1" in errs, errs
+        # a list overflow on ONE shard: every rank's merge of the gathered records returns -1
+        allr = wd.all_gather(torch.from_numpy(group_list_record(xk, xs, xc, CAP, count=bad)))
+        assert (group_merge_lists_emulated(allr.numpy(), world, CAP, None, 0) == -1) == (world > 1)
         cap_small = wd.group_exchange_error(wd.group_slot_counts(
             torch.from_numpy(group_slots_emulated(win, xk, xs, xc, 1, 0, 64)), 1, 64), 3)
         assert (cap_small is not None) == (len(xk) > 3)

@@ -87,18 +87,12 @@ def test_group_slots_match_oracle(shards, S, key_lo):
         lists.append((xk[:nx], xs[:nx], xc[:nx]))
     rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", "price < 35")
     ok, os_, oc, g = _combine_slots(total, shards, S, key_lo)
-    if g == wx.GROUP_NEEDS_MERGE:  # some shard's groups outgrew its slot: the variable-size merge
+    if g == wx.GROUP_NEEDS_MERGE:  # some shard's groups outgrew its slot: the list-record merge
         assert max(x[0].numel() for x in lists) > S
-        k = torch.cat([a for a, _, _ in lists]).long()
-        s = torch.cat([b for _, b, _ in lists])
-        c = torch.cat([c for _, _, c in lists])
-        uk, inv = torch.unique(k, sorted=True, return_inverse=True)
-        ms = torch.zeros(uk.numel(), dtype=torch.float64, device="cuda").index_add_(0, inv, s)
-        mc = torch.zeros(uk.numel(), dtype=torch.int64, device="cuda").index_add_(0, inv, c)
-        m = uk.numel()
-        g = wx.group_combine(total.data_ptr(), key_lo, uk.int().contiguous().data_ptr() if m else 0,
-                             ms.data_ptr() if m else 0, mc.data_ptr() if m else 0, m, launch(), 1 << 14,
-                             ok.data_ptr(), os_.data_ptr(), oc.data_ptr(), want_count=True)
+        cap = 1 << 14
+        recs = _list_records([(a.cpu().numpy(), b.cpu().numpy(), c.cpu().numpy()) for a, b, c in lists], cap)
+        g = wx.group_merge_lists(recs.data_ptr(), shards, cap, total.data_ptr(), key_lo, launch(), cap,
+                                 ok.data_ptr(), os_.data_ptr(), oc.data_ptr(), want_count=True)
     else:
         assert max(x[0].numel() for x in lists) <= S
     assert np.array_equal(ok[:g].cpu().numpy(), rk) and np.array_equal(oc[:g].cpu().numpy(), rc)
@@ -160,6 +154,154 @@ def test_group_slots_bad_arguments():
         with pytest.raises(wx.WarpExecError) as e:
             wx.group_combine_slots(ex.data_ptr(), world, S, 0, launch(), 0, 0, 0, 0)
         assert e.value.status == wx.WX_ERR_INVALID
+
+
+def _list_records(groups, cap, counts=None):
+    """Gathered group list records (wx_group_merge_lists layout) on the
+    device from per-list (keys, sums, counts) arrays; counts[r] overrides a
+    record's count word."""
+    nbytes, so, co = wx.group_list_layout(cap)
+    buf = np.zeros(max(1, len(groups)) * nbytes, np.uint8)
+    for r, (k, sm, c) in enumerate(groups):
+        rec = buf[r * nbytes:(r + 1) * nbytes]
+        m = len(k)
+        cw = m if counts is None or counts[r] is None else counts[r]
+        rec[0:8] = np.array([cw], np.int64).view(np.uint8)
+        rec[8:8 + 4 * m] = np.asarray(k, np.int32).view(np.uint8)
+        rec[so:so + 8 * m] = np.asarray(sm, np.float64).view(np.uint8)
+        rec[co:co + 8 * m] = np.asarray(c, np.int64).view(np.uint8)
+    return torch.from_numpy(buf).cuda()
+
+
+def _merge_lists_ref(groups, window=None, key_lo=0):
+    """wx_group_merge_lists' contract: equal keys summed in list order (the
+    first list's sum, then the others added), merged with the non-empty bins
+    of the window (ascending keys)."""
+    acc = {}
+    for k, sm, c in groups:
+        for j in range(len(k)):
+            a = acc.get(int(k[j]))
+            acc[int(k[j])] = [float(sm[j]), int(c[j])] if a is None else [a[0] + float(sm[j]), a[1] + int(c[j])]
+    if window is not None:
+        for b in range(W):
+            if window[W + b] != 0.0:
+                assert key_lo + b not in acc
+                acc[key_lo + b] = [float(window[b]), int(window[W + b])]
+    ks = sorted(acc)
+    return (np.array(ks, np.int64), np.array([acc[x][0] for x in ks], np.float64),
+            np.array([acc[x][1] for x in ks], np.int64))
+
+
+def _merge_lists(recs, n_lists, cap, window=None, key_lo=0, capacity=1 << 16):
+    ok = torch.full((max(1, capacity),), -7, dtype=torch.int32, device="cuda")
+    os_ = torch.empty(max(1, capacity), dtype=torch.float64, device="cuda")
+    oc = torch.empty(max(1, capacity), dtype=torch.int64, device="cuda")
+    ng = torch.empty(1, dtype=torch.int64, device="cuda")
+    wx.group_merge_lists(recs.data_ptr(), n_lists, cap, window.data_ptr() if window is not None else 0, key_lo,
+                         launch(), capacity, ok.data_ptr(), os_.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr())
+    torch.cuda.synchronize()
+    return ok, os_, oc, int(ng.item())
+
+
+def _random_lists(rng, n_lists, cap, lo, hi, window_lo=None):
+    """n_lists sorted unique key lists of random length <= cap over [lo, hi),
+    none inside [window_lo, window_lo + W); random sums (signs, magnitudes)."""
+    out = []
+    for _ in range(n_lists):
+        m = int(rng.integers(0, cap + 1))
+        pool = np.arange(lo, hi, dtype=np.int64)
+        if window_lo is not None:
+            pool = pool[(pool < window_lo) | (pool >= window_lo + W)]
+        m = min(m, pool.size)
+        k = np.sort(rng.choice(pool, m, replace=False))
+        sm = rng.standard_normal(m) * 10.0 ** rng.integers(-3, 12, m)
+        c = rng.integers(1, 1 << 40, m)
+        out.append((k, sm, c))
+    return out
+
+
+@pytest.mark.parametrize("n_lists,cap", [(1, 1), (1, 1000), (2, 7), (3, 1000), (8, 5000), (64, 300), (17, 1)])
+@pytest.mark.parametrize("with_window", [False, True])
+def test_group_merge_lists_matches_reference(n_lists, cap, with_window):
+    """Random overlapping sorted lists (some empty), with and without a
+    window: keys, counts and sum BITS equal the list-order reference."""
+    rng = np.random.default_rng(n_lists * 1000 + cap + with_window)
+    key_lo = int(rng.integers(-3000, 3000)) if with_window else 0
+    groups = _random_lists(rng, n_lists, cap, -6000, 6000, key_lo if with_window else None)
+    window = None
+    if with_window:
+        w = np.zeros(2 * W + 1)
+        used = rng.random(W) < 0.3
+        w[:W][used] = rng.standard_normal(int(used.sum())) * 1e6
+        w[W:2 * W][used] = rng.integers(1, 1000, int(used.sum()))
+        window = torch.from_numpy(w).cuda()
+    recs = _list_records(groups, cap)
+    ok, os_, oc, g = _merge_lists(recs, n_lists, cap, window, key_lo)
+    rk, rs, rc = _merge_lists_ref(groups, window.cpu().numpy() if window is not None else None, key_lo)
+    assert g == len(rk)
+    assert np.array_equal(ok[:g].cpu().numpy(), rk) and np.array_equal(oc[:g].cpu().numpy(), rc)
+    assert np.array_equal(os_[:g].cpu().numpy().view(np.uint64), rs.view(np.uint64))  # bit for bit, list order
+    again = _merge_lists(recs, n_lists, cap, window, key_lo)  # deterministic
+    assert again[3] == g and torch.equal(again[1][:g], os_[:g])
+
+
+def test_group_merge_lists_bad_counts_and_capacity():
+    rng = np.random.default_rng(3)
+    groups = _random_lists(rng, 4, 100, 0, 1000)
+    for bad in (-1, 101, 1 << 40):  # a shard whose table / list overflowed: -1 for everyone
+        recs = _list_records(groups, 100, counts=[None, bad, None, None])
+        assert _merge_lists(recs, 4, 100)[3] == -1
+        with pytest.raises(wx.WarpExecError) as e:
+            wx.group_merge_lists(recs.data_ptr(), 4, 100, 0, 0, launch(), 1 << 10, 0, 0, 0, want_count=True)
+        assert e.value.status == wx.WX_ERR_CAPACITY
+    # fewer output slots than groups: the first `capacity` written, the full count reported
+    recs = _list_records(groups, 100)
+    rk, rs, rc = _merge_lists_ref(groups)
+    ok, os_, oc, g = _merge_lists(recs, 4, 100, capacity=5)
+    assert g == len(rk) and np.array_equal(ok[:5].cpu().numpy(), rk[:5])
+    with pytest.raises(wx.WarpExecError) as e:
+        wx.group_merge_lists(recs.data_ptr(), 4, 100, 0, 0, launch(), 5, ok.data_ptr(), os_.data_ptr(),
+                             oc.data_ptr(), want_count=True)
+    assert e.value.status == wx.WX_ERR_CAPACITY
+    # all lists empty, window only
+    w = np.zeros(2 * W + 1)
+    w[[0, 5, W - 1]] = [1.5, -2.0, 3.0]
+    w[[W, W + 5, 2 * W - 1]] = [1, 2, 3]
+    recs = _list_records([(np.zeros(0), np.zeros(0), np.zeros(0))] * 3, 10)
+    ok, os_, oc, g = _merge_lists(recs, 3, 10, torch.from_numpy(w).cuda(), -100)
+    assert g == 3 and ok[:3].cpu().tolist() == [-100, -95, -100 + W - 1] and os_[:3].cpu().tolist() == [1.5, -2.0, 3.0]
+    for n_lists, cap in ((0, 10), (1025, 1), (2, 0)):
+        with pytest.raises(wx.WarpExecError) as e:
+            wx.group_merge_lists(recs.data_ptr(), n_lists, cap, 0, 0, launch(), 0, 0, 0, 0)
+        assert e.value.status == wx.WX_ERR_INVALID
+
+
+@pytest.mark.parametrize("shards", [1, 2, 5, 8])
+def test_group_merge_lists_many_keys_against_oracle(shards, monkeypatch):
+    """The many-key row-sharded GROUP BY as ShardedQuery.group_sum_lists runs
+    it: every shard's whole wx_group_sum (the range-partitioned kernels above
+    2^20 rows) written into its list record, the records gathered, merged on
+    the device -- against the oracle over the whole table (2^21 + 7 rows,
+    200 000 distinct keys)."""
+    monkeypatch.setenv("WARPDB_GP_MIN_ROWS", "1")
+    n = (1 << 21) + 7
+    cols = {"price": synth.uniform_f32(n, 1, 0.0, 40.0),
+            "quantity": synth.uniform_int(n, 3, -100_000, 99_999).astype(np.int32)}
+    cap = 1 << 18
+    nbytes, so, co = wx.group_list_layout(cap)
+    recs = torch.zeros(shards * nbytes, dtype=torch.uint8, device="cuda")
+    for r, (_, t) in enumerate(_shard_views(cols, shards)):
+        rec = recs[r * nbytes:(r + 1) * nbytes]
+        if t is None:
+            continue  # an empty shard: count 0
+        wx.group_sum(t, "price[idx]", "quantity[idx]", "(price[idx] < 30.0f)", launch(), 0, cap,
+                     rec[8:8 + 4 * cap].view(torch.int32).data_ptr(), rec[so:so + 8 * cap].view(torch.float64).data_ptr(),
+                     rec[co:co + 8 * cap].view(torch.int64).data_ptr(), d_n_groups=rec[0:8].view(torch.int64).data_ptr())
+    ok, os_, oc, g = _merge_lists(recs, shards, cap, capacity=cap)
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", "price < 30")
+    assert g == len(rk)
+    assert np.array_equal(ok[:g].cpu().numpy(), rk) and np.array_equal(oc[:g].cpu().numpy(), rc)
+    np.testing.assert_allclose(os_[:g].cpu().numpy(), rs, rtol=1e-12, atol=0)
 
 
 def _records(host, shards, k, desc, cond=None, select=None):
@@ -226,6 +368,7 @@ def _ngpus():
     ("sum", ["--total-rows", "40000001"]),
     ("group", ["--rows", "1e7"]),
     ("group", ["--total-rows", "2e7"]),
+    ("group", ["--rows", "4e6", "--keys", "100000"]),  # many keys: list records, one all-gather, the list merge
     ("topk", ["--rows", "1e7"]),
 ])
 def test_bench_rccl_ranks(workload, extra):
@@ -258,7 +401,8 @@ def _bench_ranks(n, workload, extra, env_extra=None):
     ("project", ["--rows", "1e7", "--c4-rows", "20000001", "--c3-rows", "10000001"]),
     ("sum", ["--total-rows", "20000001"]),
     ("group", ["--rows", "1e7"]),
-    ("group", ["--rows", "3e6", "--keys", "3000"]),  # keys beyond the window: slots, then the -2 merge
+    ("group", ["--rows", "3e6", "--keys", "3000"]),  # keys beyond the window: the list records and merge
+    ("group", ["--rows", "4e6", "--keys", "100000"]),  # the range-partitioned shard GROUP BY into the records
     ("topk", ["--rows", "1e7"]),
 ])
 def test_bench_rccl_one_rank(workload, extra):

@@ -1,0 +1,20 @@
+#!/usr/bin/env bash
+# Round 3, session 2: the many-key list merge (wx_group_merge_lists) -- its
+# GPU tests, the exchange / multi-shard tests around it, the many-key
+# multi-rank bench on a one-rank RCCL communicator, and a kernel trace of the
+# strong-scaled C3 step at its 8-GPU per-rank size (1.25e8 rows).
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+O=$R/gpurun_out/s3
+mkdir -p "$O"
+timeout -k 10 900 python3 -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu_exchange.py \
+  tests/test_gpu_multi.py -k "merge_lists or slots or one_rank or one_device or virtual or resident" > "$O/pytest.log" 2>&1
+export RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29561 WARPDB_EXCHANGE_ONE_RANK=1
+timeout -k 10 300 python3 bench.py --workload group --keys 1000000 --steps 10 --warmup 3 --no-cpu-baseline \
+  > "$O/bench_group_1e6k_lists_rccl1.json" 2> "$O/bench_group_1e6k_lists_rccl1.err"
+cd /tmp && export TMPDIR=/tmp
+MASTER_PORT=29562 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c3s" -o run --output-format csv -- \
+  python3 "$R/bench.py" --workload group --total-rows 1.25e8 --steps 200 --warmup 20 --no-cpu-baseline \
+  > "$O/prof_c3s.log" 2>&1
+echo done

@@ -48,6 +48,15 @@ def group_slots_doubles(n_slots: int, slot_groups: int) -> int:
     """WX_GROUP_SLOTS_DOUBLES: the one-collective GROUP BY exchange buffer."""
     return GROUP_EXCHANGE_DOUBLES + n_slots * (1 + 3 * slot_groups)
 
+
+def group_list_layout(cap: int):
+    """WX_GROUP_LIST_*: (record bytes, sums offset, counts offset) of one
+    shard's group list record (int64 count | int32 keys[cap] padded to 8 B |
+    f64 sums[cap] | int64 counts[cap])."""
+    sums_off = 8 + 8 * ((cap + 1) // 2)
+    counts_off = sums_off + 8 * cap
+    return counts_off + 8 * cap, sums_off, counts_off
+
 MODE_DENSE = 0
 MODE_DENSE_FILL = 1
 MODE_COMPACT = 2
@@ -64,6 +73,7 @@ EXPORTED_SYMBOLS = (
     "wx_group_combine",
     "wx_group_partials_slots",
     "wx_group_combine_slots",
+    "wx_group_merge_lists",
     "wx_topk_merge",
     "wx_cast",
     "wx_topk",
@@ -143,6 +153,7 @@ def load() -> ctypes.CDLL:
         "wx_group_partials_slots": [T, E, E, E, L, I32, P, I32, I32, I32, I64, P, P, P, P, pI64, E, S],
         "wx_group_combine_slots": [P, I32, I32, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_topk_merge": [P, I32, I32, I32, L, P, P, P, P, pI64, E, S],
+        "wx_group_merge_lists": [P, I32, I64, P, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_cast": [P, I32, P, I32, I64, L, E, S],
         "wx_topk": [T, E, E, E, I32, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_sort_pairs": [P, P, I64, I32, L, E, S],
@@ -351,6 +362,22 @@ def group_combine_slots(d_exchange: int, n_slots: int, slot_groups: int, key_win
     st = lib.wx_group_combine_slots(d_exchange, n_slots, slot_groups, key_window_lo, ctypes.byref(launch), capacity,
                                     d_keys or None, d_sums or None, d_counts or None, d_n_groups or None,
                                     ctypes.byref(h) if want_count else None, err, len(err))
+    _check(st, err)
+    return h.value if want_count else None
+
+
+def group_merge_lists(d_lists: int, n_lists: int, list_capacity: int, d_window: int, key_window_lo: int,
+                      launch: WxLaunch, capacity: int, d_keys: int, d_sums: int, d_counts: int, d_n_groups: int = 0,
+                      want_count: bool = False) -> Optional[int]:
+    """Final groups from n_lists gathered group list records (device; see
+    group_list_layout), merged with the combined window d_window (0: none).
+    The count is -1 when a list's count was negative or above list_capacity."""
+    lib = load()
+    err = _err()
+    h = ctypes.c_int64(-1)
+    st = lib.wx_group_merge_lists(d_lists or None, n_lists, list_capacity, d_window or None, key_window_lo,
+                                  ctypes.byref(launch), capacity, d_keys or None, d_sums or None, d_counts or None,
+                                  d_n_groups or None, ctypes.byref(h) if want_count else None, err, len(err))
     _check(st, err)
     return h.value if want_count else None
 

@@ -220,6 +220,36 @@ struct WxGroupCombineArgs {
   wx_i64 *n_groups_out;
 };
 
+// Many-key row-sharded GROUP BY (wx_group_merge_lists): n_lists gathered
+// list records (count, then list_cap keys / sums / counts, ascending unique
+// keys) merged in (key, list) order into scratch, then the runs of equal keys
+// summed in list order and merged with the (optional) combined window.
+#define WX_GLIST_BLOCK 1024
+#define WX_GLIST_PER 4  // merged positions per thread in the count / emit kernels
+#define WX_GLIST_SPAN (WX_GLIST_BLOCK * WX_GLIST_PER)
+struct WxGroupListsArgs {
+  const unsigned char *lists;  // n_lists x list_bytes
+  wx_i64 list_bytes;
+  wx_i64 list_cap;
+  wx_i64 sums_off;    // byte offsets inside one record
+  wx_i64 counts_off;
+  int n_lists;
+  int key_lo;
+  const double *window;  // nullable: [2 * WX_GROUP_WINDOW + 1] combined window
+  int *m_keys;           // scratch [n_lists * list_cap], merged order
+  double *m_sums;
+  wx_i64 *m_cnts;
+  wx_u32 *m_head;  // 1: first of its key in merged order
+  wx_i64 *blk;     // [n_blk] heads per WX_GLIST_SPAN positions -> exclusive prefix
+  wx_i64 n_blk;
+  wx_i64 *meta;  // [0] merged elements, [1] unique keys below key_lo, [2] non-empty window bins, [3] status
+  int *out_keys;
+  double *out_sums;
+  wx_i64 *out_counts;
+  wx_i64 capacity;
+  wx_i64 *n_groups_out;  // -1: a list's count was negative or above list_cap
+};
+
 // General-key entries -> (key ^ sign) << 32 | used-list position, padded
 // with ~0 to npad, for the device-wide sort of a large GROUP BY.
 struct WxGroupGatherArgs {

@@ -2781,6 +2781,263 @@ extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine_sl
   wx_group_combine_body(c, s_wtot + 0, &s_nlo);
 }
 
+// Many-key row-sharded GROUP BY (wx_group_merge_lists; replaces a host merge
+// of the shards' groups, src/multi_gpu_utils.cpp:23-60 gathers on the host):
+// every shard's groups arrive as one fixed-size list record (ascending unique
+// keys) from ONE all-gather.  wx_glist_place puts each group at its place in
+// (key, list) order -- its index in its own list plus, per other list, the
+// groups with a smaller key (and, from an earlier list, an equal one), found
+// by binary search -- and marks the first group of each key; wx_glist_count
+// counts those heads per WX_GLIST_SPAN places; wx_glist_scan turns the counts
+// into offsets, places the window's groups and publishes the totals;
+// wx_glist_emit sums each run of equal keys in list order (every rank adds
+// them alike) and writes the unique groups below and above the window's.
+static_assert(WX_GROUP_WINDOW == 2 * WX_GLIST_BLOCK, "two window bins per list-merge thread");
+__device__ __forceinline__ wx_i64 wx_gl_raw(const WxGroupListsArgs &a, int r) {
+  return *reinterpret_cast<const wx_i64 *>(a.lists + (wx_i64)r * a.list_bytes);
+}
+__device__ __forceinline__ wx_i64 wx_gl_valid(const WxGroupListsArgs &a, int r) {  // a bad count reads as empty
+  const wx_i64 c = wx_gl_raw(a, r);
+  return (c < 0 || c > a.list_cap) ? 0 : c;
+}
+__device__ __forceinline__ const int *wx_gl_keys(const WxGroupListsArgs &a, int r) {
+  return reinterpret_cast<const int *>(a.lists + (wx_i64)r * a.list_bytes + 8);
+}
+__device__ __forceinline__ wx_i64 wx_gl_lower(const int *keys, wx_i64 n, int k) {  // keys[0..n) below k
+  wx_i64 lo = 0, hi = n;
+  while (lo < hi) {
+    const wx_i64 mid = (lo + hi) >> 1;
+    if (keys[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ wx_i64 wx_gl_merged(const WxGroupListsArgs &a) {
+  wx_i64 m = 0;
+  for (int r = 0; r < a.n_lists; ++r) m += wx_gl_valid(a, r);
+  return m;
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_glist_place(WxGroupListsArgs a) {
+  const wx_i64 total = (wx_i64)a.n_lists * a.list_cap;
+  for (wx_i64 q = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; q < total; q += (wx_i64)gridDim.x * WX_BLOCK) {
+    const int r = (int)(q / a.list_cap);
+    const wx_i64 i = q - (wx_i64)r * a.list_cap;
+    if (i >= wx_gl_valid(a, r)) continue;
+    const unsigned char *rec = a.lists + (wx_i64)r * a.list_bytes;
+    const int k = wx_gl_keys(a, r)[i];
+    wx_i64 pos = i;
+    bool head = true;
+    for (int s = 0; s < a.n_lists; ++s) {
+      if (s == r) continue;
+      const int *ks = wx_gl_keys(a, s);
+      const wx_i64 ns = wx_gl_valid(a, s);
+      const wx_i64 lb = wx_gl_lower(ks, ns, k);
+      const bool eq = lb < ns && ks[lb] == k;
+      if (s < r) {
+        pos += lb + (eq ? 1 : 0);
+        head = head && !eq;
+      } else {
+        pos += lb;
+      }
+    }
+    a.m_keys[pos] = k;
+    a.m_sums[pos] = reinterpret_cast<const double *>(rec + a.sums_off)[i];
+    a.m_cnts[pos] = reinterpret_cast<const wx_i64 *>(rec + a.counts_off)[i];
+    a.m_head[pos] = head ? 1u : 0u;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_GLIST_BLOCK) void wx_glist_count(WxGroupListsArgs a) {
+  __shared__ wx_u32 s_w[WX_GLIST_BLOCK / 64];
+  __shared__ wx_i64 s_m;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_m = wx_gl_merged(a);
+  __syncthreads();
+  const wx_i64 m = s_m;
+  const wx_i64 p0 = (wx_i64)blockIdx.x * WX_GLIST_SPAN + (wx_i64)tid * WX_GLIST_PER;
+  wx_u32 c = 0u;
+#pragma unroll
+  for (int j = 0; j < WX_GLIST_PER; ++j)
+    if (p0 + j < m) c += a.m_head[p0 + j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((tid & 63) == 0) s_w[tid >> 6] = c;
+  __syncthreads();
+  if (tid == 0) {
+    wx_i64 t = 0;
+    for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) t += s_w[w];
+    a.blk[blockIdx.x] = t;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_GLIST_BLOCK) void wx_glist_scan(WxGroupListsArgs a) {
+  __shared__ wx_i64 s_w[WX_GLIST_BLOCK / 64];
+  __shared__ wx_i64 s_carry, s_p0, s_pb;
+  __shared__ int s_bad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) {
+    s_carry = 0;
+    s_p0 = 0;
+    s_pb = 0;
+    s_bad = 0;
+  }
+  __syncthreads();
+  // list validity, and P0 = groups with a key below the window (their places come first)
+  for (int r = tid; r < a.n_lists; r += WX_GLIST_BLOCK) {
+    const wx_i64 c = wx_gl_raw(a, r);
+    if (c < 0 || c > a.list_cap) atomicOr(&s_bad, 1);
+    if (a.window)
+      atomicAdd(reinterpret_cast<unsigned long long *>(&s_p0),
+                (unsigned long long)wx_gl_lower(wx_gl_keys(a, r), wx_gl_valid(a, r), a.key_lo));
+  }
+  __syncthreads();
+  const wx_i64 p0 = s_p0;
+  const wx_i64 b0 = p0 / WX_GLIST_SPAN;
+  // exclusive prefix of the per-span head counts, 1024 spans per round
+  for (wx_i64 base = 0; base < a.n_blk; base += WX_GLIST_BLOCK) {
+    const wx_i64 i = base + tid;
+    const wx_i64 v = i < a.n_blk ? a.blk[i] : 0;
+    wx_i64 incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_i64 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    wx_i64 wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) {
+      const wx_i64 x = s_w[w];
+      wb += w < wave ? x : 0;
+      tot += x;
+    }
+    const wx_i64 carry = s_carry;
+    if (i < a.n_blk) {
+      a.blk[i] = carry + wb + incl - v;
+      if (i == b0) s_pb = carry + wb + incl - v;
+    }
+    __syncthreads();
+    if (tid == 0) s_carry = carry + tot;
+    __syncthreads();
+  }
+  const wx_i64 U = s_carry;  // unique keys over all lists
+  // unique keys below the window: the heads before place P0
+  wx_i64 nlo = 0;
+  if (a.window) {
+    if (b0 >= a.n_blk) {
+      nlo = U;
+    } else {
+      const wx_i64 q0 = b0 * WX_GLIST_SPAN + (wx_i64)tid * WX_GLIST_PER;
+      wx_u32 c = 0u;
+#pragma unroll
+      for (int j = 0; j < WX_GLIST_PER; ++j)
+        if (q0 + j < p0) c += a.m_head[q0 + j];
+      wx_i64 cc = c;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cc += __shfl_xor(cc, o);
+      if (lane == 0) s_w[wave] = cc;
+      __syncthreads();
+      nlo = s_pb;
+      for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) nlo += s_w[w];
+      __syncthreads();
+    }
+  }
+  // the window's non-empty bins, in key order, between the groups below and above it
+  wx_i64 wn = 0;
+  if (a.window) {
+    const int b = 2 * tid;
+    const double c0 = a.window[WX_GROUP_WINDOW + b], c1 = a.window[WX_GROUP_WINDOW + b + 1];
+    const wx_u32 f = (c0 != 0.0 ? 1u : 0u) + (c1 != 0.0 ? 1u : 0u);
+    wx_u32 incl = f;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_u32 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    wx_i64 wb = 0;
+#pragma unroll
+    for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) {
+      wb += w < wave ? s_w[w] : 0;
+      wn += s_w[w];
+    }
+    wx_i64 pos = nlo + wb + incl - f;
+    if (!s_bad) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double c = h ? c1 : c0;
+        if (c == 0.0) continue;
+        if (pos < a.capacity) {
+          a.out_keys[pos] = a.key_lo + b + h;
+          a.out_sums[pos] = a.window[b + h];
+          a.out_counts[pos] = (wx_i64)c;
+        }
+        ++pos;
+      }
+    }
+  }
+  if (tid == 0) {
+    a.meta[0] = wx_gl_merged(a);
+    a.meta[1] = nlo;
+    a.meta[2] = wn;
+    a.meta[3] = s_bad ? -1 : 0;
+    *a.n_groups_out = s_bad ? -1 : U + wn;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_GLIST_BLOCK) void wx_glist_emit(WxGroupListsArgs a) {
+  __shared__ wx_u32 s_w[WX_GLIST_BLOCK / 64];
+  __shared__ wx_i64 s_m;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (a.meta[3] != 0) return;  // a bad list: the scan reported -1, nothing is written
+  if (tid == 0) s_m = a.meta[0];
+  const wx_i64 nlo = a.meta[1], wn = a.meta[2];
+  __syncthreads();
+  const wx_i64 m = s_m;
+  const wx_i64 p0 = (wx_i64)blockIdx.x * WX_GLIST_SPAN + (wx_i64)tid * WX_GLIST_PER;
+  wx_u32 hm = 0u, nh = 0u;
+#pragma unroll
+  for (int j = 0; j < WX_GLIST_PER; ++j)
+    if (p0 + j < m && a.m_head[p0 + j]) {
+      hm |= 1u << j;
+      ++nh;
+    }
+  wx_u32 incl = nh;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const wx_u32 t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  wx_i64 wb = 0;
+#pragma unroll
+  for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) wb += w < wave ? s_w[w] : 0u;
+  wx_i64 u = a.blk[blockIdx.x] + wb + incl - nh;
+#pragma unroll
+  for (int j = 0; j < WX_GLIST_PER; ++j) {
+    if (!(hm & (1u << j))) continue;
+    const wx_i64 p = p0 + j;
+    const int k = a.m_keys[p];
+    double sum = a.m_sums[p];  // list order: the first list's sum, then the others' added
+    wx_i64 cnt = a.m_cnts[p];
+    for (wx_i64 q = p + 1; q < m && a.m_keys[q] == k; ++q) {
+      sum += a.m_sums[q];
+      cnt += a.m_cnts[q];
+    }
+    const wx_i64 idx = u < nlo ? u : u + wn;
+    if (idx < a.capacity) {
+      a.out_keys[idx] = k;
+      a.out_sums[idx] = sum;
+      a.out_counts[idx] = cnt;
+    }
+    ++u;
+  }
+}
+
 // Global ORDER BY .. LIMIT k of a row-sharded query from every shard's
 // candidates (wx_topk_merge): n_records records of <= k (key, value, row)
 // candidates each.  A candidate's place is the number of candidates that

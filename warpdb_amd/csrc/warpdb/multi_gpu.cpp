@@ -218,6 +218,43 @@ Comms &comms_for(int ndev) {
 
 namespace {
 
+// ncclAllGather of `bytes` bytes per shard: every shard's `recv` receives
+// all shards' `send` buffers in shard order (co-located virtual shards go
+// through the host; one shard copies unless the one-rank test hook is on).
+void allgather_bytes(const std::vector<ShardRange> &shards, const std::vector<void *> &send,
+                     const std::vector<void *> &recv, const std::vector<hipStream_t> &streams, size_t bytes) {
+  const size_t ns = shards.size();
+  if (ns == 1 && !exchange_one_rank()) {
+    DevGuard g(shards[0].device);
+    hip_ok(hipMemcpyAsync(recv[0], send[0], bytes, hipMemcpyDeviceToDevice, streams[0]), "hipMemcpyAsync");
+    return;
+  }
+  if (ns > 1 && !distinct_devices(shards)) {
+    std::vector<char> all(bytes * ns);
+    for (size_t i = 0; i < ns; ++i) {
+      DevGuard g(shards[i].device);
+      hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
+      hip_ok(hipMemcpy(all.data() + bytes * i, send[i], bytes, hipMemcpyDeviceToHost), "hipMemcpy");
+    }
+    for (size_t i = 0; i < ns; ++i) {
+      DevGuard g(shards[i].device);
+      hip_ok(hipMemcpy(recv[i], all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    }
+    return;
+  }
+  Comms &cm = comms_for(static_cast<int>(ns));
+  std::lock_guard<std::mutex> clk(cm.mu);
+  if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
+  for (size_t i = 0; i < ns; ++i) {
+    DevGuard g(shards[i].device);
+    if (ncclAllGather(send[i], recv[i], bytes, ncclUint8, cm.comms[i], streams[i]) != ncclSuccess) {
+      (void)ncclGroupEnd();
+      throw std::runtime_error("ncclAllGather failed");
+    }
+  }
+  if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("RCCL all-gather failed");
+}
+
 // In-place ncclAllReduce(SUM, ncclFloat64) of `count` doubles of every
 // shard's buffer, one call per device inside one group (devices 0..n-1, as
 // plan_shards assigns them).  A single shard has nothing to exchange.
@@ -313,7 +350,16 @@ std::pair<double, int64_t> run_multi_gpu_sum(const HostTable &host, const std::s
 struct GroupScratch {
   int64_t cap = 0;
   size_t win_doubles = 0;  // the one-collective exchange buffer (window + slots)
-  DeviceBuffer win, xk, xs, xc, nx, ok, os, oc, ng;
+  int lists = 0;           // records `all` holds
+  // rec: this shard's out-of-window groups as one list record
+  // (WX_GROUP_LIST_BYTES(cap): count | keys | sums | counts); all: every
+  // shard's record after the all-gather of the many-key fallback
+  DeviceBuffer win, rec, all, ok, os, oc, ng;
+  char *r() const { return static_cast<char *>(rec.ptr); }
+  int32_t *xk() const { return reinterpret_cast<int32_t *>(r() + 8); }
+  double *xs() const { return reinterpret_cast<double *>(r() + WX_GROUP_LIST_SUMS_OFF(cap)); }
+  int64_t *xc() const { return reinterpret_cast<int64_t *>(r() + WX_GROUP_LIST_COUNTS_OFF(cap)); }
+  int64_t *nx() const { return reinterpret_cast<int64_t *>(r()); }
 };
 
 // Per-shard top-K candidates and their all-gathered copies (k <= 32).
@@ -545,8 +591,10 @@ std::pair<double, int64_t> ResidentShards::sum(const std::string &expr_cuda, con
 // up to 64 out-of-window groups, zeros in the others), ONE ncclAllReduce of
 // the exchange buffers (it reduces the windows and gathers the slots), then
 // wx_group_combine_slots on the first shard's device.  Only when a shard had
-// more out-of-window groups than its slot holds (WX_GROUP_NEEDS_MERGE) are
-// those groups read back from every shard and merged on the host.
+// more out-of-window groups than its slot holds (WX_GROUP_NEEDS_MERGE) does a
+// second collective follow: an all-gather of every shard's whole list of
+// out-of-window groups (one fixed-size record each), merged with the window
+// by wx_group_merge_lists on the first shard's device.
 GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::string &key_cuda,
                                       const std::string &cond_cuda, int32_t key_lo) const {
   std::lock_guard<std::mutex> lk(impl_->mu);
@@ -569,10 +617,7 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
       g.win_doubles = WD;
     }
     if (g.cap < kCap) {
-      g.xk = DeviceBuffer(r.device, kCap * 4);
-      g.xs = DeviceBuffer(r.device, kCap * 8);
-      g.xc = DeviceBuffer(r.device, kCap * 8);
-      g.nx = DeviceBuffer(r.device, 8);
+      g.rec = DeviceBuffer(r.device, static_cast<size_t>(WX_GROUP_LIST_BYTES(kCap)));
       g.ok = DeviceBuffer(r.device, kCap * 4);
       g.os = DeviceBuffer(r.device, kCap * 8);
       g.oc = DeviceBuffer(r.device, kCap * 8);
@@ -585,9 +630,8 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
     char err[8192];
     throw_on(wx_group_partials_slots(&v.table, val_cuda.c_str(), key_cuda.c_str(), cond_cuda.c_str(), &L, key_lo,
                                      static_cast<double *>(g.win.ptr), static_cast<int32_t>(ns),
-                                     static_cast<int32_t>(i), S, kCap, static_cast<int32_t *>(g.xk.ptr),
-                                     static_cast<double *>(g.xs.ptr), static_cast<int64_t *>(g.xc.ptr),
-                                     static_cast<int64_t *>(g.nx.ptr), nullptr, err, sizeof(err)),
+                                     static_cast<int32_t>(i), S, kCap, g.xk(), g.xs(), g.xc(), g.nx(), nullptr, err,
+                                     sizeof(err)),
              err);
     wins[i] = static_cast<double *>(g.win.ptr);
   });
@@ -635,52 +679,29 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
   if (ng == -1) throw std::runtime_error("group table / output capacity exceeded (general-key table overflow)");
   if (shard_err) std::rethrow_exception(shard_err);
   const bool merged_extra = ng == WX_GROUP_NEEDS_MERGE;
-  DeviceBuffer mk, ms, mc;
   if (merged_extra) {
-    std::map<int32_t, std::pair<double, int64_t>> merged;
+    // every shard's whole out-of-window list (already in its record): ONE
+    // all-gather of the fixed-size records, merged with the combined window
+    // on the first shard's device (wx_group_merge_lists)
+    const size_t rb = static_cast<size_t>(WX_GROUP_LIST_BYTES(kCap));
+    std::vector<void *> send(ns), recv(ns);
     for (size_t i = 0; i < ns; ++i) {
       GroupScratch &g = impl_->group[i];
-      DevGuard dg(ranges[i].device);
-      int64_t nx = 0;
-      hip_ok(hipMemcpy(&nx, g.nx.ptr, 8, hipMemcpyDeviceToHost), "hipMemcpy");
-      std::vector<int32_t> k(nx);
-      std::vector<double> sm(nx);
-      std::vector<int64_t> c(nx);
-      if (nx) {
-        hip_ok(hipMemcpy(k.data(), g.xk.ptr, nx * 4, hipMemcpyDeviceToHost), "hipMemcpy");
-        hip_ok(hipMemcpy(sm.data(), g.xs.ptr, nx * 8, hipMemcpyDeviceToHost), "hipMemcpy");
-        hip_ok(hipMemcpy(c.data(), g.xc.ptr, nx * 8, hipMemcpyDeviceToHost), "hipMemcpy");
+      if (g.lists != static_cast<int>(ns)) {
+        g.all = DeviceBuffer(ranges[i].device, rb * ns);
+        g.lists = static_cast<int>(ns);
       }
-      for (int64_t j = 0; j < nx; ++j) {
-        auto &e = merged[k[j]];
-        e.first += sm[j];
-        e.second += c[j];
-      }
+      send[i] = g.rec.ptr;
+      recv[i] = g.all.ptr;
     }
-    const int64_t m = static_cast<int64_t>(merged.size());
-    std::vector<int32_t> k;
-    std::vector<double> sm;
-    std::vector<int64_t> c;
-    for (auto &e : merged) {
-      k.push_back(e.first);
-      sm.push_back(e.second.first);
-      c.push_back(e.second.second);
-    }
-    mk = DeviceBuffer(dev0, m * 4);
-    ms = DeviceBuffer(dev0, m * 8);
-    mc = DeviceBuffer(dev0, m * 8);
+    allgather_bytes(ranges, send, recv, streams, rb);
     DevGuard dg(dev0);
-    hip_ok(hipMemcpy(mk.ptr, k.data(), m * 4, hipMemcpyHostToDevice), "hipMemcpy");
-    hip_ok(hipMemcpy(ms.ptr, sm.data(), m * 8, hipMemcpyHostToDevice), "hipMemcpy");
-    hip_ok(hipMemcpy(mc.ptr, c.data(), m * 8, hipMemcpyHostToDevice), "hipMemcpy");
     wx_launch L = sync_launch(dev0, streams[0]);
-    throw_on(wx_group_combine(static_cast<double *>(g0.win.ptr), key_lo, static_cast<int32_t *>(mk.ptr),
-                              static_cast<double *>(ms.ptr), static_cast<int64_t *>(mc.ptr), m, &L, kCap,
-                              static_cast<int32_t *>(g0.ok.ptr), static_cast<double *>(g0.os.ptr),
-                              static_cast<int64_t *>(g0.oc.ptr), static_cast<int64_t *>(g0.ng.ptr), nullptr, err,
-                              sizeof(err)),
+    throw_on(wx_group_merge_lists(g0.all.ptr, static_cast<int32_t>(ns), kCap, static_cast<double *>(g0.win.ptr), key_lo,
+                                  &L, kCap, static_cast<int32_t *>(g0.ok.ptr), static_cast<double *>(g0.os.ptr),
+                                  static_cast<int64_t *>(g0.oc.ptr), static_cast<int64_t *>(g0.ng.ptr), &ng, err,
+                                  sizeof(err)),
              err);
-    hip_ok(hipMemcpy(&ng, g0.ng.ptr, 8, hipMemcpyDeviceToHost), "hipMemcpy");  // combined again: the new count
   }
   DevGuard dg(dev0);
   if (ng > kCap) throw std::runtime_error("group table / output capacity exceeded");

@@ -17,8 +17,10 @@ the C ABI.  The exchanges are the ones the result needs, one collective each
                elsewhere, so the same SUM both reduces the window and gathers
                the slots; wx_group_combine_slots merges them on the device.
                Only when a shard had more out-of-window groups than its slot
-               holds (every rank sees it in the same combined buffer) does a
-               variable-size all-gather merge follow
+               holds (every rank sees it in the same combined buffer) does an
+               all-gather of every shard's fixed-size group list record
+               follow, merged by wx_group_merge_lists on the device; with
+               many keys (group_sum_lists) that all-gather is the exchange
   top-K        all-gather of one 520-byte wx_topk_record per shard (K keys,
                values, global rows, count), merged by wx_topk_merge on the
                device (better key, NaN last, then the smaller row)
@@ -173,33 +175,6 @@ def group_exchange_error(counts: List[int], capacity: int) -> Optional[str]:
     return None
 
 
-def _gather_padded(t: torch.Tensor, n: int, group=None) -> Tuple[torch.Tensor, List[int]]:
-    """All-gather the first n entries of t from every rank (variable n)."""
-    world = _world(group)
-    dev = _dev(group)
-    sizes = all_gather(torch.tensor([n], dtype=torch.int64, device=dev), group).cpu().tolist()
-    m = max(1, max(sizes))
-    buf = torch.zeros(m, dtype=t.dtype, device=dev)
-    if n:
-        buf[:n] = t[:n].to(dev)
-    out = all_gather(buf, group)
-    parts = [out[r * m: r * m + sizes[r]] for r in range(world)]
-    return torch.cat(parts), sizes
-
-
-def merge_groups(keys: torch.Tensor, sums: torch.Tensor, counts: torch.Tensor, n: int, group=None):
-    """Combine per-shard (key, sum, count) groups by key; ascending keys, float64 sums.
-
-    The fallback for keys outside the dense window (and the general merge)."""
-    k, _ = _gather_padded(keys.to(torch.int64), n, group)
-    s, _ = _gather_padded(sums.to(torch.float64), n, group)
-    c, _ = _gather_padded(counts.to(torch.int64), n, group)
-    uk, inv = torch.unique(k, sorted=True, return_inverse=True)
-    ss = torch.zeros(uk.numel(), dtype=torch.float64, device=k.device).index_add_(0, inv, s)
-    cc = torch.zeros(uk.numel(), dtype=torch.int64, device=k.device).index_add_(0, inv, c)
-    return uk.to(torch.int32), ss, cc
-
-
 # ------------------------------------------------------------------ top-K
 TOPK_MAX = 32
 TOPK_RECORD_BYTES = TOPK_MAX * 16 + 8  # wx_topk_record (include/warpexec.h)
@@ -318,13 +293,22 @@ class ShardedQuery:
         return float(h[0]), int(h[1])
 
     # --- GROUP BY ---------------------------------------------------------
+    def _group_record(self, capacity: int):
+        """This shard's group list record (wx_group_merge_lists layout) and
+        its (keys, sums, counts, count) views."""
+        nbytes, so, co = self.wx.group_list_layout(capacity)
+        rec = self._buf("grec", nbytes, torch.uint8)[:nbytes]
+        return (rec, rec[8:8 + 4 * capacity].view(torch.int32), rec[so:so + 8 * capacity].view(torch.float64),
+                rec[co:co + 8 * capacity].view(torch.int64), rec[0:8].view(torch.int64))
+
     def _group_bufs(self, capacity: int):
+        """Exchange buffer and the out-of-window groups, written straight into
+        this shard's list record (the many-key fallback gathers it as is)."""
         wx = self.wx
         S = group_slot_groups(self.world)
         nd = wx.group_slots_doubles(self.world, S)
-        return (S, self._buf("gex", nd, torch.float64)[:nd], self._buf("gxk", capacity, torch.int32),
-                self._buf("gxs", capacity, torch.float64), self._buf("gxc", capacity, torch.int64),
-                self._buf("gnx", 1, torch.int64), self._buf("gok", capacity, torch.int32),
+        _, xk, xs, xc, nx = self._group_record(capacity)
+        return (S, self._buf("gex", nd, torch.float64)[:nd], xk, xs, xc, nx, self._buf("gok", capacity, torch.int32),
                 self._buf("gos", capacity, torch.float64), self._buf("goc", capacity, torch.int64),
                 self._buf("gng", 1, torch.int64))
 
@@ -353,6 +337,40 @@ class ShardedQuery:
                                osm.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr())
         return ok, osm, oc, ng
 
+    def group_sum_lists_device(self, val_expr: str, key_expr: str, cond: Optional[str], capacity: int = 1 << 20):
+        """GROUP BY with many distinct keys per shard: every shard's groups
+        (wx_group_sum -- the range-partitioned kernels for a wide key range)
+        written straight into its list record, ONE all-gather of the records,
+        and wx_group_merge_lists on the device.  No window and no slots; the
+        only host reads are the local key-range probe of wx_group_sum.
+        Returns (keys, sums, counts, n_groups) device tensors of `capacity`
+        entries; n_groups is -1 on every rank when some shard had more than
+        `capacity` groups."""
+        wx = self.wx
+        rec, xk, xs, xc, nx = self._group_record(capacity)
+        ok, osm, oc = (self._buf("gok", capacity, torch.int32), self._buf("gos", capacity, torch.float64),
+                       self._buf("goc", capacity, torch.int64))
+        ng = self._buf("gng", 1, torch.int64)
+        wx.group_sum(self.table, val_expr, key_expr, cond, self.launch, 0, capacity, xk.data_ptr(), xs.data_ptr(),
+                     xc.data_ptr(), d_n_groups=nx.data_ptr(), want_count=False)
+        lists = all_gather(rec, self.group) if self.exchange else rec
+        wx.group_merge_lists(lists.data_ptr(), self.world if self.exchange else 1, capacity, 0, 0, self.launch_aux,
+                             capacity, ok.data_ptr(), osm.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr())
+        return ok, osm, oc, ng
+
+    def group_sum_lists(self, val_expr: str, key_expr: str, cond: Optional[str], capacity: int = 1 << 20):
+        """group_sum_lists_device with the groups returned (ascending keys)."""
+        ok, osm, oc, ng = self.group_sum_lists_device(val_expr, key_expr, cond, capacity)
+        n = int(ng.item())
+        try:
+            self.wx.check(self.launch)
+        except self.wx.WarpExecError:
+            if n >= 0:
+                raise
+        if n < 0 or n > capacity:
+            raise self.wx.WarpExecError(self.wx.WX_ERR_CAPACITY, f"groups exceed capacity {capacity} on some shard")
+        return ok[:n].clone(), osm[:n].clone(), oc[:n].clone()
+
     def group_sum(self, val_expr: str, key_expr: str, cond: Optional[str], key_lo: int = 0,
                   capacity: int = 1 << 16):
         """GROUP BY over every shard as device tensors of the final groups.
@@ -373,13 +391,14 @@ class ShardedQuery:
                     pass
                 raise wx.WarpExecError(wx.WX_ERR_CAPACITY, err)
             if n == wx.GROUP_NEEDS_MERGE:  # some shard's out-of-window groups outgrew its slot
-                m = int(counts[_rank(self.group)])
-                mk, ms, mc = merge_groups(xk, xs, xc, m, self.group)
-                mk, ms, mc = mk.cuda(), ms.cuda(), mc.cuda()
-                # identical merged groups on every rank: a capacity error is raised by all of them
-                n = wx.group_combine(ex.data_ptr(), key_lo, mk.data_ptr(), ms.data_ptr(), mc.data_ptr(), mk.numel(),
-                                     self.launch_aux, capacity, ok.data_ptr(), osm.data_ptr(), oc.data_ptr(),
-                                     d_n_groups=ng.data_ptr(), want_count=True)
+                # every shard's whole out-of-window list (already in its record):
+                # one all-gather, merged with the combined window on the device
+                rec = self._group_record(capacity)[0]
+                lists = all_gather(rec, self.group)
+                # identical records on every rank: a capacity error is raised by all of them
+                n = wx.group_merge_lists(lists.data_ptr(), self.world, capacity, ex.data_ptr(), key_lo,
+                                         self.launch_aux, capacity, ok.data_ptr(), osm.data_ptr(), oc.data_ptr(),
+                                         d_n_groups=ng.data_ptr(), want_count=True)
         self.wx.check(self.launch)
         if n > capacity or n < 0:
             raise self.wx.WarpExecError(self.wx.WX_ERR_CAPACITY, f"{n} groups exceed capacity {capacity}")
