@@ -17,4 +17,9 @@ cd /tmp && export TMPDIR=/tmp
 MASTER_PORT=29562 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$O/prof_c3s" -o run --output-format csv -- \
   python3 "$R/bench.py" --workload group --total-rows 1.25e8 --steps 200 --warmup 20 --no-cpu-baseline \
   > "$O/prof_c3s.log" 2>&1
+cd "$R"
+unset RANK WORLD_SIZE LOCAL_RANK MASTER_ADDR MASTER_PORT WARPDB_EXCHANGE_ONE_RANK
+# radix sort: per-tile phase times of every pass (diagnostic build)
+AB_ROUNDS=1 timeout -k 10 300 python3 tools/ab_sort_rank.py 1e9 keys 0 "WX_RS_DIAG_PHASES=1" \
+  > "$O/sort_phases.txt" 2>&1
 echo done

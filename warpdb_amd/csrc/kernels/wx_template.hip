@@ -4116,9 +4116,36 @@ __device__ __forceinline__ void wx_rs_payload(const WxRadixPassArgs &a, int tile
 // latencies.  (A persistent variant that loaded the next tile during this
 // one's look-back needed 161 VGPRs, ran one workgroup per CU and took 33 ms
 // per 1e9 keys against 20.7 ms here: profiles/r01/bench_sort_variants.txt.)
+#ifndef WX_RS_DIAG_PHASES
+// diagnostic: thread 0 stamps s_memrealtime (10 ns) at the phase boundaries
+// of every tile -- entry, ticket, keys landed (an extra vmcnt(0) wait), ranked,
+// offsets resolved (look-back), permuted, stores issued, stores done (an extra
+// wait) -- summed per pass over the tiles in control words 64.. (u64); the
+// last tile of a pass prints the per-tile averages
+#define WX_RS_DIAG_PHASES 0
+#endif
+#if WX_RS_DIAG_PHASES
+#define WX_RS_STAMP(i) \
+  do {                   \
+    if (threadIdx.x == 0) ts[i] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define WX_RS_VMWAIT() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+#else
+#define WX_RS_STAMP(i) \
+  do {                   \
+  } while (0)
+#define WX_RS_VMWAIT() \
+  do {                   \
+  } while (0)
+#endif
+
 template <bool PAY, int KIND, bool ASC>
 __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#if WX_RS_DIAG_PHASES
+  wx_u64 ts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  WX_RS_STAMP(0);
   if (tid == 0) S.tk[0] = atomicAdd(&a.ctl[0], 1u);
   wx_u64 *peers = reinterpret_cast<wx_u64 *>(s_k);
   for (int i = tid; i < WX_RS_WAVES * 256; i += WX_RS_BLOCK) (&S.wc[0][0])[i] = 0u;
@@ -4130,9 +4157,13 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
   const wx_i64 wb = tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane;
   const int tile_n = a.n - tb < WX_RS_TILE ? (int)(a.n - tb) : WX_RS_TILE;
   wx_u32 x[WX_RS_ITEMS], v[WX_RS_ITEMS], rk[WX_RS_ITEMS], pos[WX_RS_ITEMS], gdst[WX_RS_ITEMS];
+  WX_RS_STAMP(1);
   wx_rs_load<PAY>(a, wb, tb + WX_RS_TILE <= a.n, x, v);
+  WX_RS_VMWAIT();
+  WX_RS_STAMP(2);
   wx_rs_rank<KIND, ASC>(a, S, peers, wb, x, rk);
   __syncthreads();
+  WX_RS_STAMP(3);
   if (WX_RS_SPLIT) {
     const wx_u32 tot = wx_rs_local(a, S, tile);
     __syncthreads();  // S.ld
@@ -4147,11 +4178,33 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
     else
       wx_rs_digits(a, S, tile);
     __syncthreads();
+    WX_RS_STAMP(4);
     wx_rs_scatter<KIND, ASC>(a, S, wb, x, rk, pos, s_k);
   }
   __syncthreads();
+  WX_RS_STAMP(5);
   wx_rs_store<KIND, ASC>(a, S, tile_n, s_k, gdst);
   if (PAY) wx_rs_payload(a, tile_n, wb, v, pos, gdst, s_k);
+  WX_RS_STAMP(6);
+  WX_RS_VMWAIT();
+  WX_RS_STAMP(7);
+#if WX_RS_DIAG_PHASES
+  if (tid == 0) {
+    unsigned long long *st = reinterpret_cast<unsigned long long *>(a.ctl - 2 * (a.shift / 8) + 64) + 8 * (a.shift / 8);
+    for (int i = 0; i < 7; ++i) atomicAdd(&st[i], (unsigned long long)(ts[i + 1] - ts[i]));
+    __threadfence();
+    const wx_u32 nt = (wx_u32)((a.n + WX_RS_TILE - 1) / WX_RS_TILE);
+    if (atomicAdd(reinterpret_cast<unsigned int *>(&st[7]), 1u) == nt - 1u) {
+      __threadfence();
+      printf("[rsphase] pass %d tiles %u per-tile us: ticket %.3f load %.3f rank %.3f digits+lookback %.3f "
+             "scatter %.3f store-issue %.3f store-drain %.3f\n",
+             a.shift / 8, nt, atomicAdd(&st[0], 0ull) * 0.01 / nt, atomicAdd(&st[1], 0ull) * 0.01 / nt,
+             atomicAdd(&st[2], 0ull) * 0.01 / nt, atomicAdd(&st[3], 0ull) * 0.01 / nt,
+             atomicAdd(&st[4], 0ull) * 0.01 / nt, atomicAdd(&st[5], 0ull) * 0.01 / nt,
+             atomicAdd(&st[6], 0ull) * 0.01 / nt);
+    }
+  }
+#endif
 }
 
 #ifndef WX_RS_MINW
