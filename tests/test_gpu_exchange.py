@@ -252,7 +252,7 @@ def test_group_merge_lists_bad_counts_and_capacity():
         recs = _list_records(groups, 100, counts=[None, bad, None, None])
         assert _merge_lists(recs, 4, 100)[3] == -1
         with pytest.raises(wx.WarpExecError) as e:
-            wx.group_merge_lists(recs.data_ptr(), 4, 100, 0, 0, launch(), 1 << 10, 0, 0, 0, want_count=True)
+            wx.group_merge_lists(recs.data_ptr(), 4, 100, 0, 0, launch(), 0, 0, 0, 0, want_count=True)
         assert e.value.status == wx.WX_ERR_CAPACITY
     # fewer output slots than groups: the first `capacity` written, the full count reported
     recs = _list_records(groups, 100)
