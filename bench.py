@@ -336,7 +336,7 @@ def self_check(workload, sq, cols, n, world, wd, torch, out_v=None, keys=1024):
             raise SystemExit(f"check failed: SUM {got_s} / {got_c} vs {float(want[0])} / {int(want[1])}")
         return f"ok: count {got_c} exact, sum {got_s:.6e} within 1e-12"
     if workload == "group":
-        if keys > wx.GROUP_WINDOW_BINS:  # the timed many-key form: list records + wx_group_merge_lists
+        if keys > wd.GROUP_WINDOW_BINS:  # the timed many-key form: list records + wx_group_merge_lists
             gk, gs, gc = sq.group_sum_lists(expr, aux, None, group_capacity(keys))
         else:
             gk, gs, gc = sq.group_sum(expr, aux, None, 0, group_capacity(keys))
