@@ -49,7 +49,7 @@ def check():
     return "ok"
 
 
-ENV_KNOBS = ("WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW")
+ENV_KNOBS = ("WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW", "WARPDB_RS_PLAIN")
 
 
 def apply(v):

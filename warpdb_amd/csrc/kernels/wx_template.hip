@@ -3234,6 +3234,12 @@ __device__ __forceinline__ wx_u32 wx_rs_key_t(wx_u32 x) {
   if constexpr (KIND == 0) {
     r = wx::f2ord(__uint_as_float(x));
     if (r == 0u) return 0xffffffffu;  // NaN last in either direction
+  } else if constexpr (KIND == 2) {
+    // floats with no NaN and no -0.0 (the histogram pass checked): the plain
+    // order flip, equal to f2ord on every such value, in 2 VALU ops where
+    // f2ord's zero and NaN fixes take 9 -- the tile kernels recompute the
+    // digit three times per key
+    r = x ^ ((wx_u32)((int)x >> 31) | 0x80000000u);
   } else {
     r = x ^ 0x80000000u;
   }
@@ -3278,17 +3284,19 @@ __device__ __forceinline__ void wx_rs_count(wx_u32 *h, wx_u32 x, int lane, int c
 // different banks and never one address -- no digit distribution conflicts.
 #define WX_RS_HBLOCK 1024
 #define WX_RS_HC 32
+// returns 1 for a float key the plain order flip would misplace (NaN, -0.0)
 template <int KIND, bool ASC>
-__device__ __forceinline__ void wx_rs_count_wide(wx_u32 *h, wx_u32 x, int copy) {
+__device__ __forceinline__ wx_u32 wx_rs_count_wide(wx_u32 *h, wx_u32 x, int copy) {
   const wx_u32 k = wx_rs_key_t<KIND, ASC>(x);
 #pragma unroll
   for (int p = 0; p < 4; ++p) atomicAdd(&h[(p * 256 + ((k >> (8 * p)) & 255u)) * WX_RS_HC + copy], 1u);
+  return KIND == 0 ? (wx_u32)((x & 0x7fffffffu) > 0x7f800000u || x == 0x80000000u) : 0u;
 }
-#define WX_RS_COUNT(x) wx_rs_count_wide<KIND, ASC>(h, (x), copy)
+#define WX_RS_COUNT(x) (wx_sp |= wx_rs_count_wide<KIND, ASC>(h, (x), copy))
 #else
 #define WX_RS_HBLOCK WX_BLOCK
 #define WX_RS_HC WX_RS_HCOPIES
-#define WX_RS_COUNT(x) wx_rs_count<KIND, ASC>(h, (x), lane, copy)
+#define WX_RS_COUNT(x) (wx_sp = 1u, wx_rs_count<KIND, ASC>(h, (x), lane, copy))  // no check: the general map
 #endif
 
 // All four digit histograms in one read: contiguous spans of 16-byte loads
@@ -3302,6 +3310,7 @@ __device__ __forceinline__ void wx_radix_hist_impl(const WxRadixHistArgs &a) {
   const int lane = threadIdx.x & 63;
   const int copy = lane % WX_RS_HC;
   (void)lane;
+  wx_u32 wx_sp = 0u;  // this thread saw a NaN or -0.0 key
   if (a.aligned) {
     typedef wx_u32 u4 __attribute__((ext_vector_type(4)));
     const u4 *q = reinterpret_cast<const u4 *>(a.src);
@@ -3375,6 +3384,7 @@ __device__ __forceinline__ void wx_radix_hist_impl(const WxRadixHistArgs &a) {
     for (wx_i64 i = (wx_i64)blockIdx.x * WX_RS_HBLOCK + threadIdx.x; i < a.n; i += (wx_i64)gridDim.x * WX_RS_HBLOCK)
       WX_RS_COUNT(wx::ldv(a.src + i));
   }
+  if (__builtin_amdgcn_ballot_w64(wx_sp != 0u) != 0ull && lane == 0) atomicOr(a.hist + 2048, 1u);
   __syncthreads();
   for (int i = threadIdx.x; i < 4 * 256; i += WX_RS_HBLOCK) {
     wx_u32 c = 0u;
@@ -4226,5 +4236,9 @@ WX_RS_TILEK(wx_radix_tile_kv_f_a, true, 0, true)
 WX_RS_TILEK(wx_radix_tile_kv_f_d, true, 0, false)
 WX_RS_TILEK(wx_radix_tile_kv_i_a, true, 1, true)
 WX_RS_TILEK(wx_radix_tile_kv_i_d, true, 1, false)
+WX_RS_TILEK(wx_radix_tile_k_fp_a, false, 2, true)
+WX_RS_TILEK(wx_radix_tile_k_fp_d, false, 2, false)
+WX_RS_TILEK(wx_radix_tile_kv_fp_a, true, 2, true)
+WX_RS_TILEK(wx_radix_tile_kv_fp_d, true, 2, false)
 #endif
 
