@@ -566,6 +566,31 @@ def test_sort_float_stable_nan_signed_zero(n, sort, monkeypatch):
         assert np.array_equal(bits(t.cpu().numpy()), bits(ref))
 
 
+@pytest.mark.parametrize("n", [16385, 1_000_003])
+@pytest.mark.parametrize("special", [None, "neg_zero_last", "nan_first", "neg_zero_tail"])
+def test_sort_float_plain_flip_equals_general_map(n, special, monkeypatch):
+    """The radix tiles' plain order flip (taken when the histogram pass saw no
+    NaN and no -0.0) sorts exactly as the general order map: +0.0, infinities
+    and heavy ties included; one NaN or -0.0 anywhere -- also in the last,
+    scalar-loaded elements -- makes the pass take the general map."""
+    v = _sort_input(n, 31)
+    v[np.isnan(v)] = np.float32(np.inf)
+    v[(v == 0) & np.signbit(v)] = np.float32(0.0)
+    if special == "neg_zero_last":
+        v[-1] = np.float32(-0.0)
+    elif special == "nan_first":
+        v[0] = np.float32(np.nan)
+    elif special == "neg_zero_tail":
+        v[n - (n % 4 or 1)] = np.float32(-0.0)
+    for asc in (True, False):
+        ref = v[np.argsort(v if asc else -v, kind="stable")]
+        for plain in ("1", "0"):
+            monkeypatch.setenv("WARPDB_RS_PLAIN", plain)
+            t = torch.from_numpy(v.copy()).cuda()
+            wx.sort_float(t.data_ptr(), n, asc, launch())
+            assert np.array_equal(bits(t.cpu().numpy()), bits(ref)), (plain, asc)
+
+
 @pytest.mark.parametrize("sort,n,data", [("radix", n, "mixed") for n in (1, 2, 8191, 16385, 3 * 16384 + 1, 1_000_003)]
                          + [("radix", 70_001, "constant"), ("radix", 70_001, "small_ints"),
                             ("bitonic", 8191, "mixed")])
