@@ -49,7 +49,7 @@ def check():
     return "ok"
 
 
-ENV_KNOBS = ("WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW", "WARPDB_RS_PLAIN")
+ENV_KNOBS = ("WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW", "WARPDB_RS_PLAIN", "WARPDB_RS_LEAD")
 
 
 def apply(v):

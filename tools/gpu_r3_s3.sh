@@ -13,10 +13,13 @@ PYT="python3 -u -m pytest -x -v --timeout 300 --timeout-method thread"
 timeout -k 10 900 $PYT tests/test_gpu_exchange.py tests/test_gpu_multi.py \
   -k "merge_lists or slots or one_rank or one_device or virtual or resident" > "$O/pytest.log" 2>&1
 timeout -k 10 600 $PYT tests -m gpu -k "sort or order or limit" > "$O/pytest_sort.log" 2>&1
-AB_ROUNDS=4 timeout -k 10 400 python3 tools/ab_sort_rank.py 1e9 keys 0 "WARPDB_RS_PLAIN=1;WARPDB_RS_PLAIN=0" \
-  > "$O/abl_sort_plain.txt" 2>&1
+AB_ROUNDS=4 timeout -k 10 500 python3 tools/ab_sort_rank.py 1e9 keys 0 \
+  "WARPDB_RS_PLAIN=1,WARPDB_RS_LEAD=auto;WARPDB_RS_PLAIN=0,WARPDB_RS_LEAD=auto;WARPDB_RS_PLAIN=1,WARPDB_RS_LEAD=1;WARPDB_RS_PLAIN=0,WARPDB_RS_LEAD=1" \
+  > "$O/abl_sort_plain_lead.txt" 2>&1
+AB_ROUNDS=3 timeout -k 10 400 python3 tools/ab_sort_rank.py 1e9 pairs 0 "WARPDB_RS_LEAD=auto;WARPDB_RS_LEAD=1" \
+  > "$O/abl_sort_lead_pairs.txt" 2>&1
 AB_ROUNDS=1 timeout -k 10 300 python3 tools/ab_sort_rank.py 1e9 keys 0 \
-  "WX_RS_DIAG_PHASES=1,WARPDB_RS_PLAIN=1;WX_RS_DIAG_PHASES=1,WARPDB_RS_PLAIN=0" > "$O/sort_phases.txt" 2>&1
+  "WX_RS_DIAG_PHASES=1;WX_RS_DIAG_PHASES=1,WARPDB_RS_PLAIN=0,WARPDB_RS_LEAD=1" > "$O/sort_phases.txt" 2>&1
 timeout -k 10 200 python3 bench.py --workload sort --steps 10 --no-cpu-baseline > "$O/bench_sort.json" 2> "$O/bench_sort.err"
 export RANK=0 WORLD_SIZE=1 LOCAL_RANK=0 MASTER_ADDR=127.0.0.1 MASTER_PORT=29561 WARPDB_EXCHANGE_ONE_RANK=1
 timeout -k 10 300 python3 bench.py --workload group --keys 1000000 --steps 10 --warmup 3 --no-cpu-baseline \

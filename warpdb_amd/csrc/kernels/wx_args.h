@@ -345,6 +345,7 @@ struct WxRadixPassArgs {
   int kind;
   int ascending;
   wx_u32 epoch;  // 1..WX_RS_EPOCHS
+  int lead;      // 1: rank lane 0's digit group by one ballot (a skewed digit); 0: one LDS add per key
 };
 
 struct WxSumFinArgs {

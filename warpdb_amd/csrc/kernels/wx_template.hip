@@ -3514,17 +3514,28 @@ __device__ __forceinline__ void wx_rs_load(const WxRadixPassArgs &a, wx_i64 wb, 
 
 // In-wave stable rank of each key among the wave's keys with the same digit:
 // the group's lowest lane bumps the wave's count and broadcasts the old one.
-template <int KIND, bool ASC>
+template <int KIND, bool ASC, bool WHOLE>
 __device__ __forceinline__ void wx_rs_rank(const WxRadixPassArgs &a, WxRsShared &S, wx_u64 *peers, wx_i64 wb,
                                            const wx_u32 (&x)[WX_RS_ITEMS], wx_u32 (&rk)[WX_RS_ITEMS]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const wx_u64 below = (1ull << lane) - 1ull;
 #if WX_RS_RANK_ATOMIC
   (void)peers;
+  if (!a.lead) {
+    // no skewed digit in this pass (the host read the histogram): one
+    // returning LDS add per key, nothing else
+#pragma unroll
+    for (int i = 0; i < WX_RS_ITEMS; ++i) {
+      const wx_u32 d = (wx_rs_key_t<KIND, ASC>(x[i]) >> a.shift) & 255u;
+      rk[i] = 0u;
+      if (WHOLE || wb + (wx_i64)i * 64 < a.n) rk[i] = atomicAdd(&S.wc[wave][d], 1u);
+    }
+    return;
+  }
   wx_u32 lead_bits = 0u;  // bit i: this lane is in lane 0's digit group of item i (and not lane 0)
 #pragma unroll
   for (int i = 0; i < WX_RS_ITEMS; ++i) {
-    const bool valid = wb + (wx_i64)i * 64 < a.n;
+    const bool valid = WHOLE || wb + (wx_i64)i * 64 < a.n;
     const wx_u32 d = (wx_rs_key_t<KIND, ASC>(x[i]) >> a.shift) & 255u;
     const wx_u32 d0 = __builtin_amdgcn_readfirstlane(d);
     const bool lead = valid && d == d0;
@@ -3555,7 +3566,7 @@ __device__ __forceinline__ void wx_rs_rank(const WxRadixPassArgs &a, WxRsShared 
     wx_u64 *w[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) {
-      valid[g] = wb + (wx_i64)(i + g) * 64 < a.n;
+      valid[g] = WHOLE || wb + (wx_i64)(i + g) * 64 < a.n;
       d[g] = (wx_rs_key_t<KIND, ASC>(x[i + g]) >> a.shift) & 255u;
       w[g] = peers + ((g * WX_RS_WAVES + wave) * 256 + d[g]);
     }
@@ -4058,7 +4069,7 @@ __device__ __forceinline__ void wx_rs_resolve(const WxRadixPassArgs &a, WxRsShar
 
 // Keys into digit order in LDS; pos[i] keeps each key's tile-local slot
 // (the payload follows through the same slots).
-template <int KIND, bool ASC>
+template <int KIND, bool ASC, bool WHOLE>
 __device__ __forceinline__ void wx_rs_scatter(const WxRadixPassArgs &a, WxRsShared &S, wx_i64 wb,
                                               const wx_u32 (&x)[WX_RS_ITEMS], const wx_u32 (&rk)[WX_RS_ITEMS],
                                               wx_u32 (&pos)[WX_RS_ITEMS], wx_u32 *s_k) {
@@ -4066,7 +4077,7 @@ __device__ __forceinline__ void wx_rs_scatter(const WxRadixPassArgs &a, WxRsShar
 #pragma unroll
   for (int i = 0; i < WX_RS_ITEMS; ++i) {
     wx_u32 p = 0u;
-    if (wb + (wx_i64)i * 64 < a.n) {
+    if (WHOLE || wb + (wx_i64)i * 64 < a.n) {
       const wx_u32 d = (wx_rs_key_t<KIND, ASC>(x[i]) >> a.shift) & 255u;
       p = (WX_RS_FOLD_LD ? 0u : S.ld[d]) + S.wc[wave][d] + rk[i];
       if (WX_RS_DIAG_NO_RANK) p = (wx_u32)(wave * 64 * WX_RS_ITEMS + i * 64 + (threadIdx.x & 63));
@@ -4078,14 +4089,14 @@ __device__ __forceinline__ void wx_rs_scatter(const WxRadixPassArgs &a, WxRsShar
 
 // LDS -> output: consecutive lanes write consecutive slots of a digit's run;
 // gdst[j] keeps the destination of slot j * WX_RS_BLOCK + tid for the payload.
-template <int KIND, bool ASC>
+template <int KIND, bool ASC, bool WHOLE>
 __device__ __forceinline__ void wx_rs_store(const WxRadixPassArgs &a, const WxRsShared &S, int tile_n,
                                             const wx_u32 *s_k, wx_u32 (&gdst)[WX_RS_ITEMS]) {
 #pragma unroll
   for (int j = 0; j < WX_RS_ITEMS; ++j) {
     const int pos = j * WX_RS_BLOCK + threadIdx.x;
     gdst[j] = 0u;
-    if (pos < tile_n) {
+    if (WHOLE || pos < tile_n) {
       const wx_u32 xk = s_k[pos];
       const wx_u32 d = (wx_rs_key_t<KIND, ASC>(xk) >> a.shift) & 255u;
       wx_u32 g = S.gb[d] + (wx_u32)pos;
@@ -4102,18 +4113,19 @@ __device__ __forceinline__ void wx_rs_store(const WxRadixPassArgs &a, const WxRs
 }
 
 // The payload follows its key: the same LDS slots, the same destinations.
+template <bool WHOLE>
 __device__ __forceinline__ void wx_rs_payload(const WxRadixPassArgs &a, int tile_n, wx_i64 wb,
                                               const wx_u32 (&v)[WX_RS_ITEMS], const wx_u32 (&pos)[WX_RS_ITEMS],
                                               const wx_u32 (&gdst)[WX_RS_ITEMS], wx_u32 *s_k) {
   __syncthreads();  // every key read out of s_k
 #pragma unroll
   for (int i = 0; i < WX_RS_ITEMS; ++i)
-    if (wb + (wx_i64)i * 64 < a.n) s_k[pos[i]] = v[i];
+    if (WHOLE || wb + (wx_i64)i * 64 < a.n) s_k[pos[i]] = v[i];
   __syncthreads();
 #pragma unroll
   for (int j = 0; j < WX_RS_ITEMS; ++j) {
     const int p = j * WX_RS_BLOCK + threadIdx.x;
-    if (p < tile_n) {
+    if (WHOLE || p < tile_n) {
       if (WX_RS_NT_STORE)
         __builtin_nontemporal_store(s_k[p], a.dst_v + gdst[j]);
       else
@@ -4135,12 +4147,16 @@ __device__ __forceinline__ void wx_rs_payload(const WxRadixPassArgs &a, int tile
 #define WX_RS_DIAG_PHASES 0
 #endif
 #if WX_RS_DIAG_PHASES
+#define WX_RS_TS_ARG , ts
+#define WX_RS_TS_PARAM , wx_u64 (&ts)[8]
 #define WX_RS_STAMP(i) \
   do {                   \
     if (threadIdx.x == 0) ts[i] = __builtin_amdgcn_s_memrealtime(); \
   } while (0)
 #define WX_RS_VMWAIT() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
 #else
+#define WX_RS_TS_ARG
+#define WX_RS_TS_PARAM
 #define WX_RS_STAMP(i) \
   do {                   \
   } while (0)
@@ -4148,6 +4164,10 @@ __device__ __forceinline__ void wx_rs_payload(const WxRadixPassArgs &a, int tile
   do {                   \
   } while (0)
 #endif
+
+template <bool PAY, int KIND, bool ASC, bool WHOLE>
+__device__ __forceinline__ void wx_radix_tile_body(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k,
+                                                   wx_u64 *peers, wx_u32 tile, wx_i64 tb WX_RS_TS_PARAM);
 
 template <bool PAY, int KIND, bool ASC>
 __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k) {
@@ -4164,14 +4184,25 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
   __syncthreads();
   const wx_u32 tile = S.tk[0];
   const wx_i64 tb = (wx_i64)tile * WX_RS_TILE;
-  const wx_i64 wb = tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane;
-  const int tile_n = a.n - tb < WX_RS_TILE ? (int)(a.n - tb) : WX_RS_TILE;
-  wx_u32 x[WX_RS_ITEMS], v[WX_RS_ITEMS], rk[WX_RS_ITEMS], pos[WX_RS_ITEMS], gdst[WX_RS_ITEMS];
   WX_RS_STAMP(1);
-  wx_rs_load<PAY>(a, wb, tb + WX_RS_TILE <= a.n, x, v);
+  // every tile but the last is whole: its copy of the body checks no bounds
+  if (tb + WX_RS_TILE <= a.n)
+    wx_radix_tile_body<PAY, KIND, ASC, true>(a, S, s_k, peers, tile, tb WX_RS_TS_ARG);
+  else
+    wx_radix_tile_body<PAY, KIND, ASC, false>(a, S, s_k, peers, tile, tb WX_RS_TS_ARG);
+}
+
+template <bool PAY, int KIND, bool ASC, bool WHOLE>
+__device__ __forceinline__ void wx_radix_tile_body(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k,
+                                                   wx_u64 *peers, wx_u32 tile, wx_i64 tb WX_RS_TS_PARAM) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const wx_i64 wb = tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane;
+  const int tile_n = WHOLE ? WX_RS_TILE : (int)(a.n - tb);
+  wx_u32 x[WX_RS_ITEMS], v[WX_RS_ITEMS], rk[WX_RS_ITEMS], pos[WX_RS_ITEMS], gdst[WX_RS_ITEMS];
+  wx_rs_load<PAY>(a, wb, WHOLE, x, v);
   WX_RS_VMWAIT();
   WX_RS_STAMP(2);
-  wx_rs_rank<KIND, ASC>(a, S, peers, wb, x, rk);
+  wx_rs_rank<KIND, ASC, WHOLE>(a, S, peers, wb, x, rk);
   __syncthreads();
   WX_RS_STAMP(3);
   if (WX_RS_SPLIT) {
@@ -4180,7 +4211,7 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
     wx_u64 first = 0ull;
     if (tid < 256 && tile != 0 && !WX_RS_DIAG_NO_LOOKBACK)
       first = wx::ld_agent(&a.status[(wx_u64)(tile - 1) * 256 + tid]);  // in flight during the permutation
-    wx_rs_scatter<KIND, ASC>(a, S, wb, x, rk, pos, s_k);
+    wx_rs_scatter<KIND, ASC, WHOLE>(a, S, wb, x, rk, pos, s_k);
     if (tid < 256) wx_rs_resolve(a, S, tile, tot, first);
   } else {
     if (WX_RS_LB_PAIR && !PAY && WX_RS_BLOCK == 512)
@@ -4189,12 +4220,12 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
       wx_rs_digits(a, S, tile);
     __syncthreads();
     WX_RS_STAMP(4);
-    wx_rs_scatter<KIND, ASC>(a, S, wb, x, rk, pos, s_k);
+    wx_rs_scatter<KIND, ASC, WHOLE>(a, S, wb, x, rk, pos, s_k);
   }
   __syncthreads();
   WX_RS_STAMP(5);
-  wx_rs_store<KIND, ASC>(a, S, tile_n, s_k, gdst);
-  if (PAY) wx_rs_payload(a, tile_n, wb, v, pos, gdst, s_k);
+  wx_rs_store<KIND, ASC, WHOLE>(a, S, tile_n, s_k, gdst);
+  if (PAY) wx_rs_payload<WHOLE>(a, tile_n, wb, v, pos, gdst, s_k);
   WX_RS_STAMP(6);
   WX_RS_VMWAIT();
   WX_RS_STAMP(7);
