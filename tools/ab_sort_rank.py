@@ -49,7 +49,8 @@ def check():
     return "ok"
 
 
-ENV_KNOBS = ("WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW", "WARPDB_RS_PLAIN", "WARPDB_RS_LEAD")
+ENV_KNOBS = ("WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW", "WARPDB_RS_PLAIN", "WARPDB_RS_LEAD",
+             "WARPDB_RS_PERSIST")
 
 
 def apply(v):
