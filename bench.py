@@ -550,8 +550,11 @@ def main_ranks(args):
                                                for c, t in cols.items()),
                           "index": "int32 shard-local row index" if workload == "project" else None,
                           "exchange": {"project": "all-gather int64 counts", "sum": "all-reduce 2 x f64",
-                                       "group": f"one all-reduce of {wd_group_doubles(world)} x f64 (key window + "
-                                                f"{world} slots of out-of-window groups), wx_group_combine_slots",
+                                       "group": (f"one all-reduce of {wd_group_doubles(world)} x f64 (key window + "
+                                                 f"{world} slots of out-of-window groups), wx_group_combine_slots"
+                                                 if args.keys <= 2048 else
+                                                 f"one all-gather of {world} group list records "
+                                                 f"({group_capacity(args.keys)} groups each), wx_group_merge_lists"),
                                        "topk": "all-gather 520 B per shard, wx_topk_merge",
                                        "dense": "none", "sort": "none"}[workload] if coll else "none (1 GPU)",
                           "parallelism": f"row-sharded x{world}, one process per GPU"}
