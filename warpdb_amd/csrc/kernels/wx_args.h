@@ -85,24 +85,6 @@ struct WxSumArgs {
   wx_i64 n_rows;
 };
 
-struct WxGroupArgs {
-  const void *col[WX_MAX_COLS];
-  wx_i64 n_rows;
-  double *win_sum;  // [WX_GROUP_WINDOW]
-  wx_u64 *win_cnt;  // [WX_GROUP_WINDOW]
-  wx_u64 *h_tag;    // [hcap] 0 = empty, else (u32)key | 1<<32
-  double *h_sum;    // [hcap]
-  wx_u64 *h_cnt;    // [hcap]
-  wx_u32 *h_used;   // [hcap] slots taken, in insertion order
-  wx_u64 *ctrs;     // [0] used slots, [1] error bits
-  wx_u32 *win_min;  // [WX_GROUP_WINDOW] order-mapped, ~0 = none (WX_MINMAX builds)
-  wx_u32 *win_max;  // [WX_GROUP_WINDOW] order-mapped, 0 = none
-  wx_u32 *h_min;    // [hcap]
-  wx_u32 *h_max;    // [hcap]
-  wx_u32 hmask;     // hcap - 1 (hcap a power of two)
-  int key_lo;
-};
-
 struct WxGroupFinArgs {
   double *win_sum;
   wx_u64 *win_cnt;
@@ -136,6 +118,27 @@ struct WxGroupFinArgs {
   int slot_rank;
   int slot_groups;
 };
+
+struct WxGroupArgs {
+  const void *col[WX_MAX_COLS];
+  wx_i64 n_rows;
+  double *win_sum;  // [WX_GROUP_WINDOW]
+  wx_u64 *win_cnt;  // [WX_GROUP_WINDOW]
+  wx_u64 *h_tag;    // [hcap] 0 = empty, else (u32)key | 1<<32
+  double *h_sum;    // [hcap]
+  wx_u64 *h_cnt;    // [hcap]
+  wx_u32 *h_used;   // [hcap] slots taken, in insertion order
+  wx_u64 *ctrs;     // [0] used slots, [1] error bits
+  wx_u32 *win_min;  // [WX_GROUP_WINDOW] order-mapped, ~0 = none (WX_MINMAX builds)
+  wx_u32 *win_max;  // [WX_GROUP_WINDOW] order-mapped, 0 = none
+  wx_u32 *h_min;    // [hcap]
+  wx_u32 *h_max;    // [hcap]
+  wx_u32 hmask;     // hcap - 1 (hcap a power of two)
+  int key_lo;
+  int fused;           // 1: the last workgroup runs the finalize (`fin`); ctrs[2] counts finished workgroups
+  WxGroupFinArgs fin;  // the finalize's arguments when fused
+};
+
 
 // Slot layout of the one-collective GROUP BY exchange (wx_group_partials_slots)
 #define WX_GROUP_EXCHANGE (2 * WX_GROUP_WINDOW + 1)
