@@ -250,6 +250,8 @@ class ShardedQuery:
         # secondary kernels (combines, finalizes) stay out of WX_F_TIME timing
         self.launch_aux = wx.make_launch(device=dev, stream=stream, custom_src=custom_src, flags=0)
         self._bufs = {}
+        self._gbufs = {}  # capacity -> _group_bufs views
+        self._grecs = {}  # capacity -> group list record and its views
 
     def _buf(self, name: str, n: int, dtype) -> torch.Tensor:
         b = self._bufs.get(name)
@@ -296,21 +298,32 @@ class ShardedQuery:
     def _group_record(self, capacity: int):
         """This shard's group list record (wx_group_merge_lists layout) and
         its (keys, sums, counts, count) views."""
-        nbytes, so, co = self.wx.group_list_layout(capacity)
-        rec = self._buf("grec", nbytes, torch.uint8)[:nbytes]
-        return (rec, rec[8:8 + 4 * capacity].view(torch.int32), rec[so:so + 8 * capacity].view(torch.float64),
-                rec[co:co + 8 * capacity].view(torch.int64), rec[0:8].view(torch.int64))
+        got = self._grecs.get(capacity)
+        if got is None:  # one record per capacity: cached views never outlive a reallocation
+            nbytes, so, co = self.wx.group_list_layout(capacity)
+            rec = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+            got = (rec, rec[8:8 + 4 * capacity].view(torch.int32), rec[so:so + 8 * capacity].view(torch.float64),
+                   rec[co:co + 8 * capacity].view(torch.int64), rec[0:8].view(torch.int64))
+            self._grecs[capacity] = got
+        return got
 
     def _group_bufs(self, capacity: int):
         """Exchange buffer and the out-of-window groups, written straight into
-        this shard's list record (the many-key fallback gathers it as is)."""
+        this shard's list record (the many-key fallback gathers it as is).
+        Built once per capacity: the views hold their storage, and a timed
+        multi-rank step pays no tensor slicing on the host."""
+        got = self._gbufs.get(capacity)
+        if got is not None:
+            return got
         wx = self.wx
         S = group_slot_groups(self.world)
         nd = wx.group_slots_doubles(self.world, S)
         _, xk, xs, xc, nx = self._group_record(capacity)
-        return (S, self._buf("gex", nd, torch.float64)[:nd], xk, xs, xc, nx, self._buf("gok", capacity, torch.int32),
-                self._buf("gos", capacity, torch.float64), self._buf("goc", capacity, torch.int64),
-                self._buf("gng", 1, torch.int64))
+        got = (S, self._buf("gex", nd, torch.float64)[:nd], xk, xs, xc, nx, self._buf("gok", capacity, torch.int32),
+               self._buf("gos", capacity, torch.float64), self._buf("goc", capacity, torch.int64),
+               self._buf("gng", 1, torch.int64))
+        self._gbufs[capacity] = got
+        return got
 
     def group_sum_device(self, val_expr: str, key_expr: str, cond: Optional[str], key_lo: int = 0,
                          capacity: int = 1 << 16):
