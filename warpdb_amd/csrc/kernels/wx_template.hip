@@ -4335,15 +4335,17 @@ __device__ __forceinline__ wx_u32 wx_rs_step(const WxRadixPassArgs &a, WxRsShare
   const wx_i64 tb = (wx_i64)tile * WX_RS_TILE;
   const wx_i64 wb = tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane;
   const int tile_n = WHOLE ? WX_RS_TILE : (int)(a.n - tb);
-  wx_u32 nxt = 0u;
-  if (tid == 0) nxt = atomicAdd(&a.ctl[0], 1u);  // in flight during this tile
   wx_u32 rk[WX_RS_ITEMS], pos[WX_RS_ITEMS], gdst[WX_RS_ITEMS], nov[WX_RS_ITEMS];
   wx_rs_rank<KIND, ASC, WHOLE>(a, S, nullptr, wb, x, rk);
   __syncthreads();
   wx_rs_digits(a, S, tile);
   __syncthreads();
+  // The next ticket only now, as late as the prefetch allows: a tile whose
+  // ticket is taken publishes nothing until its workgroup reaches it, and
+  // every successor's look-back waits on it (taken at the start of this
+  // tile: 46 vs 12.3 ms per 1e9 keys, profiles/r03/abl_sort_persist.txt).
+  if (tid == 0) S.tk[1] = atomicAdd(&a.ctl[0], 1u);
   wx_rs_scatter<KIND, ASC, WHOLE>(a, S, wb, x, rk, pos, s_k);
-  if (tid == 0) S.tk[1] = nxt;
   __syncthreads();
   const wx_u32 next = S.tk[1];
   if (next < nt) {  // the next tile's keys, landing while this tile's go out
