@@ -4314,82 +4314,6 @@ __device__ __forceinline__ void wx_radix_tile_body(const WxRadixPassArgs &a, WxR
 #endif
 }
 
-#ifndef WX_RS_PERSIST
-// Key tiles (no payload) in persistent workgroups: each takes its next
-// tile's ticket when it starts a tile and loads the next tile's keys into the
-// (by then free) key registers right after the permutation, so the ticket's
-// atomic and the loads' HBM latency overlap this tile's look-back and stores
-// instead of opening every tile (per-tile phase times, diagnostic build:
-// ticket 2.6 us + keys landing 4.7 us of each tile's serial path;
-// profiles/r03/sort_phases.txt).  The grid is the resident workgroups; tiles
-// stay in ticket order, so the look-back stays deadlock-free.
-#define WX_RS_PERSIST 1
-#endif
-
-// One tile of a persistent key workgroup: x holds its keys; returns the next
-// tile's ticket with that tile's keys loading into x.
-template <int KIND, bool ASC, bool WHOLE>
-__device__ __forceinline__ wx_u32 wx_rs_step(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k, wx_u32 tile,
-                                             wx_u32 nt, wx_u32 (&x)[WX_RS_ITEMS]) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const wx_i64 tb = (wx_i64)tile * WX_RS_TILE;
-  const wx_i64 wb = tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane;
-  const int tile_n = WHOLE ? WX_RS_TILE : (int)(a.n - tb);
-  wx_u32 rk[WX_RS_ITEMS], pos[WX_RS_ITEMS], gdst[WX_RS_ITEMS], nov[WX_RS_ITEMS];
-  wx_rs_rank<KIND, ASC, WHOLE>(a, S, nullptr, wb, x, rk);
-  __syncthreads();
-  wx_rs_digits(a, S, tile);
-  __syncthreads();
-  // The next ticket only now, as late as the prefetch allows: a tile whose
-  // ticket is taken publishes nothing until its workgroup reaches it, and
-  // every successor's look-back waits on it (taken at the start of this
-  // tile: 46 vs 12.3 ms per 1e9 keys, profiles/r03/abl_sort_persist.txt).
-  if (tid == 0) S.tk[1] = atomicAdd(&a.ctl[0], 1u);
-  wx_rs_scatter<KIND, ASC, WHOLE>(a, S, wb, x, rk, pos, s_k);
-  __syncthreads();
-  const wx_u32 next = S.tk[1];
-  if (next < nt) {  // the next tile's keys, landing while this tile's go out
-    const wx_i64 nb = (wx_i64)next * WX_RS_TILE;
-    wx_rs_load<false>(a, nb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane, nb + WX_RS_TILE <= a.n, x, nov);
-  }
-  wx_rs_store<KIND, ASC, WHOLE>(a, S, tile_n, s_k, gdst);
-  // the wave counts are read last by the permutation (behind the barrier above)
-  for (int i = tid; i < WX_RS_WAVES * 256; i += WX_RS_BLOCK) (&S.wc[0][0])[i] = 0u;
-  __syncthreads();
-  return next;
-}
-
-// the last, partial tile: out of line, so that its copy of the step adds no
-// registers to the loop over whole tiles
-template <int KIND, bool ASC>
-__device__ __noinline__ wx_u32 wx_rs_step_tail(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k, wx_u32 tile,
-                                               wx_u32 nt, wx_u32 (&x)[WX_RS_ITEMS]) {
-  return wx_rs_step<KIND, ASC, false>(a, S, s_k, tile, nt, x);
-}
-
-template <int KIND, bool ASC>
-__device__ __forceinline__ void wx_radix_persist_impl(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const wx_u32 nt = (wx_u32)((a.n + WX_RS_TILE - 1) / WX_RS_TILE);
-  if (tid == 0) S.tk[0] = atomicAdd(&a.ctl[0], 1u);
-  for (int i = tid; i < WX_RS_WAVES * 256; i += WX_RS_BLOCK) (&S.wc[0][0])[i] = 0u;
-  __syncthreads();
-  wx_u32 tile = S.tk[0];
-  if (tile >= nt) return;  // workgroup-uniform
-  wx_u32 x[WX_RS_ITEMS], nov[WX_RS_ITEMS];
-  {
-    const wx_i64 tb = (wx_i64)tile * WX_RS_TILE;
-    wx_rs_load<false>(a, tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane, tb + WX_RS_TILE <= a.n, x, nov);
-  }
-  while (true) {
-    const bool whole = (wx_i64)tile * WX_RS_TILE + WX_RS_TILE <= a.n;
-    const wx_u32 next = whole ? wx_rs_step<KIND, ASC, true>(a, S, s_k, tile, nt, x)
-                              : wx_rs_step_tail<KIND, ASC>(a, S, s_k, tile, nt, x);
-    if (next >= nt) break;
-    tile = next;
-  }
-}
-
 #ifndef WX_RS_MINW
 // minimum waves per SIMD the register allocation must allow: 2 workgroups
 // per CU for the 512-thread key tiles (<= 128 VGPRs), 1 for 1024 threads
@@ -4399,10 +4323,7 @@ __device__ __forceinline__ void wx_radix_persist_impl(const WxRadixPassArgs &a, 
   extern "C" __global__ __launch_bounds__(WX_RS_BLOCK, WX_RS_MINW) void NAME(WxRadixPassArgs a) { \
     __shared__ WxRsShared S;                                                            \
     __shared__ wx_u64 s_raw[WX_RS_SBUF]; /* keys / payloads; the peer masks before */ \
-    if constexpr (!PAY && WX_RS_PERSIST && WX_RS_RANK_ATOMIC && !WX_RS_SPLIT && !WX_RS_DIAG_PHASES) \
-      wx_radix_persist_impl<KIND, ASC>(a, S, reinterpret_cast<wx_u32 *>(s_raw));      \
-    else                                                                              \
-      wx_radix_tile_impl<PAY, KIND, ASC>(a, S, reinterpret_cast<wx_u32 *>(s_raw));    \
+    wx_radix_tile_impl<PAY, KIND, ASC>(a, S, reinterpret_cast<wx_u32 *>(s_raw));        \
   }
 WX_RS_TILEK(wx_radix_tile_k_f_a, false, 0, true)
 WX_RS_TILEK(wx_radix_tile_k_f_d, false, 0, false)
