@@ -3285,6 +3285,9 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApply
 #ifndef WX_RS_LBW
 #define WX_RS_LBW 2  // predecessor words per digit per look-back round (keys: 2 by 0.1-0.2 ms over 1; 8 slower)
 #endif
+#ifndef WX_RS_SLEEP
+#define WX_RS_SLEEP 1  // look-back: s_sleep between polls of an unpublished predecessor word (0: none)
+#endif
 #ifndef WX_STALL_TICKS
 #define WX_STALL_TICKS 200000000ull  // 2 s at 100 MHz without progress (see the compaction look-back)
 #endif
@@ -3859,7 +3862,7 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
 #if WX_RS_DIAG_LBSTATS
         ++lb_sleeps;
 #endif
-        __builtin_amdgcn_s_sleep(1);
+        if (WX_RS_SLEEP) __builtin_amdgcn_s_sleep(WX_RS_SLEEP);
         if ((++spins & 63u) == 0u) {
           // abort only after WX_STALL_TICKS with this digit's chain not moving
           const wx_u64 now = __builtin_amdgcn_s_memrealtime();
