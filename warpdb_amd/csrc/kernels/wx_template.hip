@@ -3283,7 +3283,10 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApply
 // and the abort word, and the launch drains.
 #define WX_RS_WAVES (WX_RS_BLOCK / 64)
 #ifndef WX_RS_LBW
-#define WX_RS_LBW 2  // predecessor words per digit per look-back round (keys: 2 by 0.1-0.2 ms over 1; 8 slower)
+// predecessor words per digit per look-back round: keys 3 (11.55 vs 11.71 ms
+// per 1e9 keys over 2, 10.22 vs 10.35 on another box, 127 VGPRs: no spill;
+// profiles/r03/abl_sort_lbw.txt, abl_sort_sleep_lbw.txt); 8 slower
+#define WX_RS_LBW 3
 #endif
 #ifndef WX_RS_SLEEP
 #define WX_RS_SLEEP 1  // look-back: s_sleep between polls of an unpublished predecessor word (0: none)
