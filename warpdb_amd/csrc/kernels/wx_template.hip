@@ -3750,49 +3750,13 @@ __device__ __forceinline__ void wx_rs_rank(const WxRadixPassArgs &a, WxRsShared 
 // inclusive {P}, publish it; fills S.gb / S.ld.  Called by every thread (it
 // holds a barrier).  Publishing before the in-tile scan and its barrier
 // rather than after: 17.0 vs 17.5 ms per 1e9 keys (ablate_sort.txt).
-#ifndef WX_RS_EARLY_A
-// 1: count the tile's digits with non-returning LDS adds (lane 0's digit
-// group by a ballot) and publish {A} BEFORE the ranking, with the first
-// look-back word in flight during it: a tile's successors wait on its {A},
-// so its latency from the ticket bounds the pass (profiles/r03/sort_phases.txt)
-#define WX_RS_EARLY_A 0
-#endif
-template <int KIND, bool ASC, bool WHOLE>
-__device__ __forceinline__ wx_u64 wx_rs_publish_early(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile,
-                                                      wx_i64 wb, const wx_u32 (&x)[WX_RS_ITEMS]) {
-  const int tid = threadIdx.x, lane = tid & 63;
-#pragma unroll
-  for (int i = 0; i < WX_RS_ITEMS; ++i) {
-    const bool valid = WHOLE || wb + (wx_i64)i * 64 < a.n;
-    const wx_u32 d = (wx_rs_key_t<KIND, ASC>(x[i]) >> a.shift) & 255u;
-    const wx_u32 d0 = __builtin_amdgcn_readfirstlane(d);
-    const bool lead = valid && d == d0;
-    const wx_u64 lm = __builtin_amdgcn_ballot_w64(lead);
-    if (valid && !lead) atomicAdd(&S.tt[d], 1u);
-    else if (lane == 0 && lm) atomicAdd(&S.tt[d0], (wx_u32)__builtin_popcountll(lm));
-  }
-  __syncthreads();
-  wx_u64 first = 0ull;
-  if (tid < 256) {
-    const wx_u64 E = (wx_u64)a.epoch << 58;
-    const bool look = tile != 0 && !WX_RS_DIAG_NO_LOOKBACK;
-    wx::st_agent(&a.status[(wx_u64)tile * 256 + tid], E | (look ? WX_RS_FLAG_A : WX_RS_FLAG_P) | S.tt[tid]);
-    if (look) first = wx::ld_agent(&a.status[(wx_u64)(tile - 1) * 256 + tid]);
-  }
-  return first;
-}
-
-// EARLY: the tile's counts {A} were published before the ranking
-// (WX_RS_EARLY_A) and `first_in` is the first predecessor word loaded then.
-template <bool EARLY = false>
-__device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile,
-                                             wx_u64 first_in = 0ull) {
+__device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const wx_u64 E = (wx_u64)a.epoch << 58;
   wx_u64 *row = a.status + (wx_u64)tile * 256;
   const bool look = tile != 0 && !WX_RS_DIAG_NO_LOOKBACK;
   wx_u32 tot = 0u, inc = 0u;
-  wx_u64 first = first_in;  // the first predecessor word, loaded before the barrier
+  wx_u64 first = 0ull;  // the first predecessor word, loaded before the barrier
   if (tid < 256) {
 #pragma unroll
     for (int w = 0; w < WX_RS_WAVES; ++w) {
@@ -3800,10 +3764,8 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
       S.wc[w][tid] = tot;
       tot += c;
     }
-    if (!EARLY) {
-      wx::st_agent(&row[tid], E | (look ? WX_RS_FLAG_A : WX_RS_FLAG_P) | tot);
-      if (WX_RS_LB_FIRST && look) first = wx::ld_agent(&a.status[(wx_u64)(tile - 1) * 256 + tid]);
-    }
+    wx::st_agent(&row[tid], E | (look ? WX_RS_FLAG_A : WX_RS_FLAG_P) | tot);
+    if (WX_RS_LB_FIRST && look) first = wx::ld_agent(&a.status[(wx_u64)(tile - 1) * 256 + tid]);
     inc = tot;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -4289,8 +4251,6 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
   if (tid == 0) S.tk[0] = atomicAdd(&a.ctl[0], 1u);
   wx_u64 *peers = reinterpret_cast<wx_u64 *>(s_k);
   for (int i = tid; i < WX_RS_WAVES * 256; i += WX_RS_BLOCK) (&S.wc[0][0])[i] = 0u;
-  if (WX_RS_EARLY_A)
-    for (int i = tid; i < 256; i += WX_RS_BLOCK) S.tt[i] = 0u;
   if (WX_RS_MATCH_LDS && !WX_RS_RANK_ATOMIC)
     for (int i = tid; i < WX_RS_RANK_G * WX_RS_WAVES * 256; i += WX_RS_BLOCK) peers[i] = 0ull;
   __syncthreads();
@@ -4314,9 +4274,6 @@ __device__ __forceinline__ void wx_radix_tile_body(const WxRadixPassArgs &a, WxR
   wx_rs_load<PAY>(a, wb, WHOLE, x, v);
   WX_RS_VMWAIT();
   WX_RS_STAMP(2);
-  wx_u64 first = 0ull;
-  if (WX_RS_EARLY_A && !WX_RS_SPLIT && !(WX_RS_LB_PAIR && !PAY && WX_RS_BLOCK == 512))
-    first = wx_rs_publish_early<KIND, ASC, WHOLE>(a, S, tile, wb, x);
   wx_rs_rank<KIND, ASC, WHOLE>(a, S, peers, wb, x, rk);
   __syncthreads();
   WX_RS_STAMP(3);
@@ -4331,8 +4288,6 @@ __device__ __forceinline__ void wx_radix_tile_body(const WxRadixPassArgs &a, WxR
   } else {
     if (WX_RS_LB_PAIR && !PAY && WX_RS_BLOCK == 512)
       wx_rs_digits_pair(a, S, tile);
-    else if (WX_RS_EARLY_A)
-      wx_rs_digits<true>(a, S, tile, first);
     else
       wx_rs_digits(a, S, tile);
     __syncthreads();
