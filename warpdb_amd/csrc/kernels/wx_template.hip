@@ -4237,18 +4237,9 @@ __device__ __forceinline__ void wx_rs_payload(const WxRadixPassArgs &a, int tile
   } while (0)
 #endif
 
-#ifndef WX_RS_SPEC
-// 1: load the keys of tile blockIdx.x while the ticket's atomic is in flight
-// and keep them when the ticket names that tile (reload otherwise): the
-// ticket is still what assigns tiles (so the look-back stays deadlock-free),
-// but its round trip overlaps the loads instead of preceding them
-#define WX_RS_SPEC 0
-#endif
-
 template <bool PAY, int KIND, bool ASC, bool WHOLE>
 __device__ __forceinline__ void wx_radix_tile_body(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k,
-                                                   wx_u64 *peers, wx_u32 tile, wx_i64 tb, wx_u32 (&x)[WX_RS_ITEMS],
-                                                   wx_u32 (&v)[WX_RS_ITEMS], bool loaded WX_RS_TS_PARAM);
+                                                   wx_u64 *peers, wx_u32 tile, wx_i64 tb WX_RS_TS_PARAM);
 
 template <bool PAY, int KIND, bool ASC>
 __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k) {
@@ -4258,12 +4249,6 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
 #endif
   WX_RS_STAMP(0);
   if (tid == 0) S.tk[0] = atomicAdd(&a.ctl[0], 1u);
-  wx_u32 x[WX_RS_ITEMS], v[WX_RS_ITEMS];
-  const wx_u32 guess = blockIdx.x;
-  if (WX_RS_SPEC) {  // the likely tile's keys, in flight with the ticket
-    const wx_i64 gb = (wx_i64)guess * WX_RS_TILE;
-    wx_rs_load<PAY>(a, gb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane, gb + WX_RS_TILE <= a.n, x, v);
-  }
   wx_u64 *peers = reinterpret_cast<wx_u64 *>(s_k);
   for (int i = tid; i < WX_RS_WAVES * 256; i += WX_RS_BLOCK) (&S.wc[0][0])[i] = 0u;
   if (WX_RS_MATCH_LDS && !WX_RS_RANK_ATOMIC)
@@ -4271,24 +4256,22 @@ __device__ __forceinline__ void wx_radix_tile_impl(const WxRadixPassArgs &a, WxR
   __syncthreads();
   const wx_u32 tile = S.tk[0];
   const wx_i64 tb = (wx_i64)tile * WX_RS_TILE;
-  const bool loaded = WX_RS_SPEC && tile == guess;  // workgroup-uniform
   WX_RS_STAMP(1);
   // every tile but the last is whole: its copy of the body checks no bounds
   if (tb + WX_RS_TILE <= a.n)
-    wx_radix_tile_body<PAY, KIND, ASC, true>(a, S, s_k, peers, tile, tb, x, v, loaded WX_RS_TS_ARG);
+    wx_radix_tile_body<PAY, KIND, ASC, true>(a, S, s_k, peers, tile, tb WX_RS_TS_ARG);
   else
-    wx_radix_tile_body<PAY, KIND, ASC, false>(a, S, s_k, peers, tile, tb, x, v, loaded WX_RS_TS_ARG);
+    wx_radix_tile_body<PAY, KIND, ASC, false>(a, S, s_k, peers, tile, tb WX_RS_TS_ARG);
 }
 
 template <bool PAY, int KIND, bool ASC, bool WHOLE>
 __device__ __forceinline__ void wx_radix_tile_body(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 *s_k,
-                                                   wx_u64 *peers, wx_u32 tile, wx_i64 tb, wx_u32 (&x)[WX_RS_ITEMS],
-                                                   wx_u32 (&v)[WX_RS_ITEMS], bool loaded WX_RS_TS_PARAM) {
+                                                   wx_u64 *peers, wx_u32 tile, wx_i64 tb WX_RS_TS_PARAM) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const wx_i64 wb = tb + (wx_i64)wave * 64 * WX_RS_ITEMS + lane;
   const int tile_n = WHOLE ? WX_RS_TILE : (int)(a.n - tb);
-  wx_u32 rk[WX_RS_ITEMS], pos[WX_RS_ITEMS], gdst[WX_RS_ITEMS];
-  if (!loaded) wx_rs_load<PAY>(a, wb, WHOLE, x, v);
+  wx_u32 x[WX_RS_ITEMS], v[WX_RS_ITEMS], rk[WX_RS_ITEMS], pos[WX_RS_ITEMS], gdst[WX_RS_ITEMS];
+  wx_rs_load<PAY>(a, wb, WHOLE, x, v);
   WX_RS_VMWAIT();
   WX_RS_STAMP(2);
   wx_rs_rank<KIND, ASC, WHOLE>(a, S, peers, wb, x, rk);
