@@ -251,7 +251,8 @@ def test_sharded_query_single_rank():
     ("project", ["--rows", "1e7", "--c4-rows", "20000001", "--c3-rows", "10000001"]),
     ("sum", ["--total-rows", "20000001"]),  # C4's strong-scaling form, ragged shards
     ("group", ["--rows", "5e6"]),           # the one-collective window + slots all-reduce
-    ("group", ["--rows", "2e6", "--keys", "3000"]),  # keys outside the window ride in the slots / the merge
+    ("group", ["--rows", "2e6", "--keys", "3000"]),  # many keys: list records, one all-gather, the device merge
+    ("group", ["--rows", "4e6", "--keys", "100000"]),  # the same over each rank's range-partitioned GROUP BY
     ("topk", ["--rows", "5e6"]),
 ])
 def test_bench_two_ranks_on_one_gpu(workload, extra):
