@@ -250,7 +250,8 @@ wx_status wx_group_combine_slots(const double *d_exchange, int32_t n_slots, int3
  * at most `capacity` written; the count goes to d_n_groups / h_n_groups.
  * It is -1 when a list's count is negative or above list_capacity (a shard
  * whose table or list overflowed): every rank sees the same records, so
- * every rank gets the same -1.  1 <= n_lists <= 1024. */
+ * every rank gets the same -1.  1 <= n_lists <= 1024, 1 <= list_capacity
+ * <= 2^31; the merge keeps 24 bytes of workspace per gathered list entry. */
 #define WX_GROUP_LIST_SUMS_OFF(cap) (8 + 8 * (((int64_t)(cap) + 1) / 2))
 #define WX_GROUP_LIST_COUNTS_OFF(cap) (WX_GROUP_LIST_SUMS_OFF(cap) + 8 * (int64_t)(cap))
 #define WX_GROUP_LIST_BYTES(cap) (WX_GROUP_LIST_COUNTS_OFF(cap) + 8 * (int64_t)(cap))
