@@ -31,6 +31,9 @@
  *                       on the host instead (src/multi_gpu_utils.cpp:5-63)
  *   wx_group_partials_slots,  the same in ONE collective: window + per-shard
  *   wx_group_combine_slots    slots of out-of-window groups (src/multi_gpu_utils.cpp:23-60)
+ *   wx_group_merge_lists  GROUP BY over row shards with many groups: the
+ *                       device merge of the shards' gathered group lists (the
+ *                       reference gathers on the host, src/multi_gpu_utils.cpp:23-60)
  *   wx_topk_merge       ORDER BY .. LIMIT over row shards: the merge of the
  *                       shards' candidate records (src/warpdb.cpp:453-455,
  *                       483-495 sort the gathered dense results instead)
