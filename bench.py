@@ -44,6 +44,12 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# Kernel arguments in device memory (a HIP runtime setting, read when HIP
+# starts, so before torch is imported): the dependent kernels of a
+# multi-rank GROUP BY step start sooner -- C3 strong at 1.25e8 rows per rank
+# 0.1688 vs 0.1723-0.1731 ms per step, the 1e9-row lines unchanged
+# (profiles/r03/s2/kernarg/).  An explicit setting in the environment wins.
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 METRIC = "rows/sec + achieved HBM GB/s, 1B-row float32 project+filter, 1/2/4/8 GPU"
@@ -63,7 +69,7 @@ WORKLOADS = {
               "wx_project_dense"),
     # ORDER BY without LIMIT (query_sql): the projection, then the radix
     # sort (jit_sort_float, src/jit.cpp:283-307); roofline over the sort
-    "sort": ("SELECT price FROM t ORDER BY price", "price[idx]", None, "wx_radix_hist + wx_radix_tile_k_f_a"),
+    "sort": ("SELECT price FROM t ORDER BY price", "price[idx]", None, "wx_radix_hist + wx_radix_tile_k_fp_a"),
 }
 # bytes every row reads from HBM (the "HBM-read roofline" of BASELINE.md)
 READ_BYTES = {"project": 8, "dense": 8, "group": 8, "sum": 4, "topk": 4, "sort": 4}
