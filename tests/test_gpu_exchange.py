@@ -460,8 +460,12 @@ def _warpdb_multi_against_oracle(tmp_path):
     s2, c2 = db.query_multi_gpu_sum("price * 0.9 WHERE price > 20")
     es2, ec2 = ora.reduce_sum(hs, "price * 0.9", "price > 20")
     assert c2 == ec2 and abs(s2 - es2) <= 1e-12 * abs(es2)
-    for sql, lo in (("SELECT SUM(price) FROM t GROUP BY quantity", 0),):
-        k, s, c = db.query_multi_gpu_group(sql)
+    # key window at 5000: all 100 keys fall outside it, more than a slot holds
+    # (-2), so the shards' group list records are all-gathered (RCCL with the
+    # one-rank hook) and merged by wx_group_merge_lists
+    for sql, lo in (("SELECT SUM(price) FROM t GROUP BY quantity", 0),
+                    ("SELECT SUM(price) FROM t GROUP BY quantity", 5000)):
+        k, s, c = db.query_multi_gpu_group(sql, lo)
         rk, rs, rc = ora.group_sum(hs, "price", "quantity")
         assert np.array_equal(k, rk) and np.array_equal(c, rc)
         np.testing.assert_allclose(s, rs, rtol=1e-12, atol=0)
