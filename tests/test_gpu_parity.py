@@ -591,6 +591,33 @@ def test_sort_float_plain_flip_equals_general_map(n, special, monkeypatch):
             assert np.array_equal(bits(t.cpu().numpy()), bits(ref)), (plain, asc)
 
 
+@pytest.mark.parametrize("n", [10241, 1_000_003])
+def test_sort_ranking_modes_agree(n, monkeypatch):
+    """The tiles' in-wave ranking by one LDS add per key (WARPDB_RS_LEAD=0),
+    with lane 0's digit group ranked by one ballot (1, the default) and chosen
+    per pass from the histogram (auto) all give the oracle's stable order:
+    float keys with heavy ties, and int key + row payload pairs whose keys
+    skew one digit (a few small values) next to a full-range digit."""
+    monkeypatch.setenv("WARPDB_SORT", "radix")
+    v = _sort_input(n, 41)
+    rng = np.random.default_rng(n)
+    keys = np.where(rng.random(n) < 0.7, rng.integers(0, 3, n), rng.integers(-2**31, 2**31 - 1, n)).astype(np.int32)
+    rows = np.arange(n, dtype=np.int32)
+    for asc in (True, False):
+        ref = v[np.argsort(v if asc else -v, kind="stable")]
+        order = np.argsort(keys if asc else -keys.astype(np.int64), kind="stable")
+        for lead in ("0", "1", "auto"):
+            monkeypatch.setenv("WARPDB_RS_LEAD", lead)
+            t = torch.from_numpy(v.copy()).cuda()
+            wx.sort_float(t.data_ptr(), n, asc, launch())
+            assert np.array_equal(bits(t.cpu().numpy()), bits(ref)), (lead, asc)
+            tk = torch.from_numpy(keys.copy()).cuda()
+            tv = torch.from_numpy(rows.copy()).cuda()
+            wx.sort_pairs(tk.data_ptr(), tv.data_ptr(), n, asc, launch())
+            assert np.array_equal(tk.cpu().numpy(), keys[order]), (lead, asc)
+            assert np.array_equal(tv.cpu().numpy(), rows[order]), (lead, asc)
+
+
 @pytest.mark.parametrize("sort,n,data", [("radix", n, "mixed") for n in (1, 2, 8191, 16385, 3 * 16384 + 1, 1_000_003)]
                          + [("radix", 70_001, "constant"), ("radix", 70_001, "small_ints"),
                             ("bitonic", 8191, "mixed")])
