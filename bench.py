@@ -29,6 +29,12 @@ one host thread and stream per device, ncclCommInitAll over devices
 0..N-1 -- WarpDB::query_multi_gpu_sum / _group / _topk), for sum, group and
 topk; its per-step time includes the collective and the host read-back.
 
+Beside the headline (`secondary`, each line timed the same way and checked
+after timing; `exchange_ms` = HIP events around the collective + device merge
+on multi-rank runs): SUM and GROUP BY on the same shards, C2 at its own 1e8
+rows per GPU, C5 (ORDER BY price DESC LIMIT 5 + discount()), and the
+strong-scaled C3 (1e9 rows) and C4 (8e9 rows) lines over all GPUs.
+
 Prints ONE JSON line (rank 0).
 """
 from __future__ import annotations
@@ -100,6 +106,10 @@ def parse():
                    help="project only: skip the strong-scaled C3 GROUP BY line (1e9 rows over all GPUs)")
     p.add_argument("--c3-rows", type=float, default=C3_TOTAL_ROWS,
                    help="rows over all GPUs of the strong-scaled C3 GROUP BY line (BASELINE: 1e9)")
+    p.add_argument("--no-c2", action="store_true", help="project only: skip the C2 line (1e8 rows per GPU)")
+    p.add_argument("--c2-rows", type=float, default=1e8, help="rows per GPU of the C2 line (BASELINE: 1e8)")
+    p.add_argument("--no-c5", action="store_true",
+                   help="project only: skip the C5 line (ORDER BY price DESC LIMIT 5 + discount())")
     p.add_argument("--keys", type=int, default=1024,
                    help="group: distinct int32 keys, uniform over [0, keys) (BASELINE C3: 1K)")
     return p.parse_args()
@@ -480,10 +490,13 @@ def main_ranks(args):
         if verbose:
             print(f"[bench rank {rank}] {what} {time.strftime('%H:%M:%S')}", file=sys.stderr, flush=True)
 
-    def timed(step_fn, warm_s=0.0):
+    def timed(step_fn, warm_s=0.0, sq_ex=None):
         """W warm-up steps (secondary lines: and at least warm_s seconds of
         them), then exactly K steps between barrier + synchronize;
-        (elapsed s, average timed-kernel ms, launches), max over ranks."""
+        (elapsed s, average timed-kernel ms, launches, exchange ms), max over
+        ranks.  With sq_ex (a ShardedQuery) the timed steps also record HIP
+        events around each exchange (collective + device merge): its average
+        is the fourth value (None on one rank)."""
         for _ in range(args.warmup):
             step_fn()
         if warm_s > 0:
@@ -504,6 +517,8 @@ def main_ranks(args):
                 step_fn()
         wx.check(L)
         wx.timing_read()  # discard the warm-up launches
+        if sq_ex is not None:
+            sq_ex.time_exchanges(args.steps)
         mark("timed steps")
         if coll:
             dist.barrier()
@@ -518,14 +533,16 @@ def main_ranks(args):
         k_ms, nl = wx.timing_read()
         wx.check(L)
         k_avg = k_ms / max(1, nl)
+        ex_ms = sq_ex.exchange_ms() if sq_ex is not None else None
         if coll:
-            t = torch.tensor([el, k_avg], dtype=torch.float64, device="cuda")
+            t = torch.tensor([el, k_avg, -1.0 if ex_ms is None else ex_ms], dtype=torch.float64, device="cuda")
             wd.all_reduce_(t, op=dist.ReduceOp.MAX)
             el, k_avg = float(t[0]), float(t[1])
-        return el, k_avg, nl
+            ex_ms = None if float(t[2]) < 0 else round(float(t[2]), 4)
+        return el, k_avg, nl, ex_ms
 
     mark("warm-up")
-    elapsed, kern_avg_ms, launches = timed(step)
+    elapsed, kern_avg_ms, launches, ex_main = timed(step, sq_ex=sq)
 
     # algorithmic bytes per launch of the dominant kernel
     passing = int(counts.item()) if workload == "project" else None
@@ -573,6 +590,8 @@ def main_ranks(args):
                                             "copy, as WarpDB::query_sql)" if src is not None
                                             else "the compacted projection")
         line["check"] = check
+        if ex_main is not None:
+            line["exchange_ms"] = ex_main
         if workload == "group":
             line["config"]["distinct_keys"] = args.keys
         line["roofline"] = roofline(bytes_per_launch, kern_avg_ms, n * rb, kname, pmc_traffic(workload, n, args.keys),
@@ -581,12 +600,31 @@ def main_ranks(args):
     # (so the driver's 1/2/4/8-GPU runs also measure SUM -- C4's 8e9 rows at
     # 8 GPUs -- and GROUP BY scaling); reported beside the headline, not in it.
     secondary = {}
+
+    def sec(key, wname, sqx, step_fn, cols_x, n_x, total_x, scaling, bytes_fn, extra=None):
+        """One checked secondary line: timed like the headline, then its own
+        self-check; `bytes_fn()` gives the dominant kernel's algorithmic
+        bytes per launch on this rank (max over ranks is the kernel time)."""
+        mark(f"secondary {key}")
+        el_x, k_ms_x, _, ex_x = timed(step_fn, SECONDARY_WARM_S, sq_ex=sqx)
+        chk_x = None if args.no_check else self_check(wname, sqx, cols_x, n_x, world, wd, torch)
+        d = {"query": WORKLOADS[wname][0]}
+        d.update(extra or {})
+        d.update({"value": round(total_x * args.steps / el_x, 1), "unit": "rows/s",
+                  "ms_per_step": round(el_x / args.steps * 1e3, 4), "scaling": scaling,
+                  "kernel": WORKLOADS[wname][3], "kernel_ms": round(k_ms_x, 4),
+                  "frac": round(bytes_fn() / (k_ms_x * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk_x})
+        if ex_x is not None:
+            d["exchange_ms"] = ex_x
+        secondary[key] = d
+
     if workload == "project" and not args.no_secondary:
+        weak = "strong" if args.total_rows else "weak"
         qk = torch.empty(max(1, n), dtype=torch.int32, device="cuda")[:n]
         wx.fill_synthetic(qk.data_ptr(), wx.INT32, n, 3, 1, 0, 1023, L, row_base=b)
         for w2, cols2 in (("sum", {"price": cols["price"]}), ("group", {"price": cols["price"], "quantity": qk})):
             sq2 = wd.ShardedQuery(wd.Shard(cols2, b, n), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
-            _, e2, a2, k2 = WORKLOADS[w2]
+            _, e2, a2, _ = WORKLOADS[w2]
             if w2 == "sum":
                 res2 = torch.zeros(2, dtype=torch.float64, device="cuda")
 
@@ -595,16 +633,38 @@ def main_ranks(args):
             else:
                 def step2():
                     sq2.group_sum_device(e2, a2, None, 0, group_capacity(1024))
-            mark(f"secondary {w2}")
-            el2, k2_ms, _ = timed(step2, SECONDARY_WARM_S)
-            chk2 = None if args.no_check else self_check(w2, sq2, cols2, n, world, wd, torch)
-            b2 = n * READ_BYTES[w2]
-            secondary[w2] = {"query": WORKLOADS[w2][0], "value": round(n_total * args.steps / el2, 1),
-                             "unit": "rows/s", "ms_per_step": round(el2 / args.steps * 1e3, 4),
-                             "scaling": line_common(args, world, n_total, el2, w2)["scaling"],
-                             "kernel": k2, "kernel_ms": round(k2_ms, 4),
-                             "frac": round(b2 / (k2_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk2}
+            sec(w2, w2, sq2, step2, cols2, n, n_total, weak, lambda: n * READ_BYTES[w2])
         del qk, sq2
+        # C2 at its own size (BASELINE configs[1]: 100M rows): the first 1e8
+        # rows of the resident columns (views, 1e8 per GPU), the same ordered
+        # compaction + the count all-gather as the headline
+        n2 = min(n, int(args.c2_rows))
+        if n2 > 0 and not args.no_c2:
+            cols2 = {"price": cols["price"][:n2], "quantity": cols["quantity"][:n2]}
+            sq2 = wd.ShardedQuery(wd.Shard(cols2, b, n2), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
+            cnt2 = torch.zeros(1, dtype=torch.int64, device="cuda")
+            _, e2, a2, _ = WORKLOADS["project"]
+
+            def step_c2():
+                sq2.compact_device(e2, a2, out_v, out_i, 4, cnt2)
+            sec("c2_1e8", "project", sq2, step_c2, cols2, n2, n2 * world, "weak",
+                lambda: n2 * 8 + int(cnt2.item()) * 8,
+                {"config": f"C2: {n2:.3g} rows per GPU (the first rows of the resident columns)",
+                 "rows_per_gpu": n2})
+            del sq2, cols2
+        # C5 (BASELINE configs[4]): ORDER BY price DESC LIMIT 5 + discount()
+        # over the 1e9-row price column on each rank; at N > 1 the record
+        # all-gather + wx_topk_merge
+        if not args.no_c5:
+            sq5 = wd.ShardedQuery(wd.Shard({"price": cols["price"]}, b, n), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
+            _, e5, a5, _ = WORKLOADS["topk"]
+
+            def step_c5():
+                sq5.topk_merged_device(e5, None, a5, 5, True)
+            sec("c5_topk", "topk", sq5, step_c5, {"price": cols["price"]}, n, n_total, weak,
+                lambda: n * READ_BYTES["topk"],
+                {"config": f"C5: {n:.3g} rows per GPU, K = 5, discount() from the custom.cu hook"})
+            del sq5
         # C3 as BASELINE states it, strong-scaled: 1e9 rows (price f32, 1K
         # int32 keys) over all ranks, 1e9 / N per GPU, each shard generated at
         # its global row numbers; GROUP BY + the one-collective exchange, so
@@ -619,19 +679,14 @@ def main_ranks(args):
             wx.fill_synthetic(k3.data_ptr(), wx.INT32, n3, 3, 1, 0, 1023, L, row_base=b3)
             cols3 = {"price": p3, "quantity": k3}
             sq3 = wd.ShardedQuery(wd.Shard(cols3, b3, n3), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
-            _, e3x, a3x, k3n = WORKLOADS["group"]
+            _, e3x, a3x, _ = WORKLOADS["group"]
 
             def step3():
                 sq3.group_sum_device(e3x, a3x, None, 0, group_capacity(1024))
-            mark("secondary c3")
-            el3, k3_ms, _ = timed(step3, SECONDARY_WARM_S)
-            chk3 = None if args.no_check else self_check("group", sq3, cols3, n3, world, wd, torch)
-            secondary["c3_group_strong"] = {
-                "query": WORKLOADS["group"][0], "config": f"C3: {c3_total:.3g} rows over all GPUs (strong scaling)",
-                "total_rows": c3_total, "rows_per_gpu": n3, "value": round(c3_total * args.steps / el3, 1),
-                "unit": "rows/s", "ms_per_step": round(el3 / args.steps * 1e3, 4), "scaling": "strong",
-                "kernel": k3n, "kernel_ms": round(k3_ms, 4),
-                "frac": round(n3 * READ_BYTES["group"] / (k3_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk3}
+            sec("c3_group_strong", "group", sq3, step3, cols3, n3, c3_total, "strong",
+                lambda: n3 * READ_BYTES["group"],
+                {"config": f"C3: {c3_total:.3g} rows over all GPUs (strong scaling)", "total_rows": c3_total,
+                 "rows_per_gpu": n3})
             del p3, k3, sq3, cols3
         # C4 exactly as BASELINE states it: 8e9 rows over all ranks (strong
         # scaling, 8e9 / N per GPU; 32 GB resident at N = 1), SUM + all-reduce,
@@ -643,20 +698,15 @@ def main_ranks(args):
             p4 = torch.empty(max(1, n4), dtype=torch.float32, device="cuda")[:n4]
             wx.fill_synthetic(p4.data_ptr(), wx.FLOAT32, n4, 1, 0, 0.0, 40.0, L, row_base=b4)
             sq4 = wd.ShardedQuery(wd.Shard({"price": p4}, b4, n4), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
-            _, e4x, a4x, k4 = WORKLOADS["sum"]
+            _, e4x, a4x, _ = WORKLOADS["sum"]
             res4 = torch.zeros(2, dtype=torch.float64, device="cuda")
 
             def step4():
                 sq4.sum_device(e4x, a4x, res4)
-            mark("secondary c4")
-            el4, k4_ms, _ = timed(step4, SECONDARY_WARM_S)
-            chk4 = None if args.no_check else self_check("sum", sq4, {"price": p4}, n4, world, wd, torch)
-            secondary["c4_sum_strong"] = {
-                "query": WORKLOADS["sum"][0], "config": f"C4: {c4_total:.3g} rows over all GPUs (strong scaling)",
-                "total_rows": c4_total, "rows_per_gpu": n4, "value": round(c4_total * args.steps / el4, 1),
-                "unit": "rows/s", "ms_per_step": round(el4 / args.steps * 1e3, 4), "scaling": "strong",
-                "kernel": k4, "kernel_ms": round(k4_ms, 4),
-                "frac": round(n4 * READ_BYTES["sum"] / (k4_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk4}
+            sec("c4_sum_strong", "sum", sq4, step4, {"price": p4}, n4, c4_total, "strong",
+                lambda: n4 * READ_BYTES["sum"],
+                {"config": f"C4: {c4_total:.3g} rows over all GPUs (strong scaling)", "total_rows": c4_total,
+                 "rows_per_gpu": n4})
             del p4, sq4
     if rank == 0:
         if secondary:

@@ -340,9 +340,11 @@ def test_bench_json_contract(args):
     assert line["scaling"] == ("strong" if "--total-rows" in args else "weak")
     if "--api" not in args:  # the bench's own post-timing check of the exchanged result
         assert str(line["check"]).startswith("ok"), line["check"]
-    if args[1] == "project":  # SUM, GROUP BY and C4's strong-scaled SUM measured beside the headline
+    if args[1] == "project":  # SUM, GROUP BY, C2, C5 and the strong-scaled C3 / C4 lines beside the headline
         sec = line["secondary"]
-        assert set(sec) == {"sum", "group", "c3_group_strong", "c4_sum_strong"}, sec
+        assert set(sec) == {"sum", "group", "c2_1e8", "c5_topk", "c3_group_strong", "c4_sum_strong"}, sec
+        assert all(0 < v["frac"] < 1.0 and v["kernel_ms"] > 0 for v in sec.values()), sec
+        assert sec["c5_topk"]["kernel"] == "wx_topk_scan" and sec["c2_1e8"]["rows_per_gpu"] == 2000003
         assert all(str(v["check"]).startswith("ok") and v["value"] > 0 for v in sec.values()), sec
         assert sec["c4_sum_strong"]["total_rows"] == 3000001 and sec["c4_sum_strong"]["scaling"] == "strong"
         assert sec["c3_group_strong"]["total_rows"] == 2000001 and sec["c3_group_strong"]["scaling"] == "strong"

@@ -1,0 +1,66 @@
+#!/usr/bin/env bash
+# The one GPU-session runner (GPU box).  Usage:
+#   bash tools/gpu_run.sh TAG STEP [STEP ...]
+# Every step runs under its own time limit, writes under gpurun_out/TAG/ and
+# stops the session on failure (set -e); steps:
+#   smoke                      __graft_entry__.smoke()
+#   suite[:PYTEST ARGS]        pytest -m gpu (--durations=25), e.g. suite:-k group
+#   bench:NAME[:BENCH ARGS]    python3 bench.py ARGS > NAME.json
+#   prof:NAME[:BENCH ARGS]     the same bench under rocprofv3 --kernel-trace --stats
+#                              (NAME_kernel_stats.csv is the summary to keep)
+#   pmc:NAME[:BENCH ARGS]      FETCH_SIZE and WRITE_SIZE passes (one counter block
+#                              each) over 3 steps, summarised to NAME_pmc.json
+#   py:NAME:SCRIPT [ARGS]      python3 SCRIPT ARGS > NAME.txt
+set -euo pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd "$R"
+TAG=$1
+shift
+O=$R/gpurun_out/$TAG
+mkdir -p "$O"
+export TMPDIR=/tmp
+for STEP in "$@"; do
+  KIND=${STEP%%:*}
+  REST=""
+  [[ "$STEP" == *:* ]] && REST=${STEP#*:}
+  NAME=${REST%%:*}
+  ARGS=""
+  [[ "$REST" == *:* ]] && ARGS=${REST#*:}
+  echo "[$(date +%T)] $STEP" | tee -a "$O/steps.log"
+  case "$KIND" in
+    smoke)
+      timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke()" > "$O/smoke.log" 2>&1 ;;
+    suite)
+      # shellcheck disable=SC2086
+      timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+        --durations=25 $REST > "$O/pytest_gpu.log" 2>&1 ;;
+    bench)
+      # shellcheck disable=SC2086
+      timeout -k 10 400 python3 bench.py $ARGS > "$O/$NAME.json" 2> "$O/$NAME.err" ;;
+    prof)
+      # shellcheck disable=SC2086
+      (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/prof_$NAME" -o run --output-format csv \
+        -- python3 "$R/bench.py" $ARGS > "$O/$NAME.json" 2> "$O/$NAME.err")
+      S=$(find "$O/prof_$NAME" -name "*kernel_stats.csv" | head -n 1 || true)
+      if [ -n "$S" ]; then cp "$S" "$O/${NAME}_kernel_stats.csv"; fi ;;
+    pmc)
+      mkdir -p "$O/pmc_$NAME"
+      for C in FETCH_SIZE WRITE_SIZE; do
+        # shellcheck disable=SC2086
+        (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc $C -d "$O/pmc_$NAME/$C" -o run --output-format csv -- \
+          python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-secondary $ARGS \
+          > "$O/pmc_$NAME/$C.log" 2>&1)
+      done
+      python3 tools/pmc_summary.py $(find "$O/pmc_$NAME" -name "*counter_collection.csv") > "$O/${NAME}_pmc.json" ;;
+    py)
+      SCRIPT=${ARGS%% *}
+      SARGS=""
+      [[ "$ARGS" == *" "* ]] && SARGS=${ARGS#* }
+      # shellcheck disable=SC2086
+      timeout -k 10 400 python3 "$SCRIPT" $SARGS > "$O/$NAME.txt" 2>&1 ;;
+    *)
+      echo "unknown step $STEP" >&2
+      exit 2 ;;
+  esac
+done
+echo "[$(date +%T)] done" | tee -a "$O/steps.log"

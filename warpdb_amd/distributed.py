@@ -252,6 +252,31 @@ class ShardedQuery:
         self._bufs = {}
         self._gbufs = {}  # capacity -> _group_bufs views
         self._grecs = {}  # capacity -> group list record and its views
+        self._ex_pool = None  # exchange timing (time_exchanges): preallocated HIP events
+        self._ex_next = 0
+
+    # --- exchange timing (bench) -------------------------------------------
+    def time_exchanges(self, steps: int) -> None:
+        """Record a HIP event pair around the exchange part (collective + the
+        device merge after it) of the next `steps` multi-rank *_device calls,
+        on the stream the launches use; read with exchange_ms()."""
+        self._ex_pool = [torch.cuda.Event(enable_timing=True) for _ in range(2 * steps)]
+        self._ex_next = 0
+
+    def _ex_mark(self) -> None:
+        if self._ex_pool is not None and self.exchange and self._ex_next < len(self._ex_pool):
+            self._ex_pool[self._ex_next].record()
+            self._ex_next += 1
+
+    def exchange_ms(self) -> Optional[float]:
+        """Average exchange time (ms) of the calls since time_exchanges; None
+        when nothing was exchanged (one shard).  Synchronises."""
+        pool, n = self._ex_pool, self._ex_next // 2
+        self._ex_pool = None
+        if not pool or n == 0:
+            return None
+        pool[2 * n - 1].synchronize()
+        return sum(pool[2 * i].elapsed_time(pool[2 * i + 1]) for i in range(n)) / n
 
     def _buf(self, name: str, n: int, dtype) -> torch.Tensor:
         b = self._bufs.get(name)
@@ -268,7 +293,10 @@ class ShardedQuery:
         self.wx.project_filter(self.table, expr, cond, self.launch, self.wx.MODE_COMPACT, vals.data_ptr(),
                                idx.data_ptr() if idx is not None else 0, idx_bytes,
                                self.shard.row_base if idx_bytes == 8 else 0, d_count=count.data_ptr())
-        return exchange_counts_device(count, self.group)
+        self._ex_mark()
+        out = exchange_counts_device(count, self.group)
+        self._ex_mark()
+        return out
 
     def compact(self, expr: str, cond: Optional[str], idx_bytes: int = 8):
         n = self.shard.n_rows
@@ -285,7 +313,10 @@ class ShardedQuery:
     def sum_device(self, expr: str, cond: Optional[str], out: torch.Tensor) -> torch.Tensor:
         """out (float64[2]) <- global {SUM(expr), COUNT} over every shard."""
         self.wx.reduce_sum(self.table, expr, cond, self.launch_sum, d_out=out.data_ptr(), want_host=False)
-        return exchange_sum_device(out, self.group)
+        self._ex_mark()
+        exchange_sum_device(out, self.group)
+        self._ex_mark()
+        return out
 
     def sum(self, expr: str, cond: Optional[str]) -> Tuple[float, int]:
         out = self._buf("sum", 2, torch.float64)[:2]
@@ -345,9 +376,11 @@ class ShardedQuery:
         wx.group_partials_slots(self.table, val_expr, key_expr, cond, self.launch, key_lo, ex.data_ptr(), self.world,
                                 _rank(self.group), S, capacity, xk.data_ptr(), xs.data_ptr(), xc.data_ptr(),
                                 d_n_extra=nx.data_ptr())
+        self._ex_mark()
         all_reduce_(ex, group=self.group)
         wx.group_combine_slots(ex.data_ptr(), self.world, S, key_lo, self.launch_aux, capacity, ok.data_ptr(),
                                osm.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr())
+        self._ex_mark()
         return ok, osm, oc, ng
 
     def group_sum_lists_device(self, val_expr: str, key_expr: str, cond: Optional[str], capacity: int = 1 << 20):
@@ -366,9 +399,11 @@ class ShardedQuery:
         ng = self._buf("gng", 1, torch.int64)
         wx.group_sum(self.table, val_expr, key_expr, cond, self.launch, 0, capacity, xk.data_ptr(), xs.data_ptr(),
                      xc.data_ptr(), d_n_groups=nx.data_ptr(), want_count=False)
+        self._ex_mark()
         lists = all_gather(rec, self.group) if self.exchange else rec
         wx.group_merge_lists(lists.data_ptr(), self.world if self.exchange else 1, capacity, 0, 0, self.launch_aux,
                              capacity, ok.data_ptr(), osm.data_ptr(), oc.data_ptr(), d_n_groups=ng.data_ptr())
+        self._ex_mark()
         return ok, osm, oc, ng
 
     def group_sum_lists(self, val_expr: str, key_expr: str, cond: Optional[str], capacity: int = 1 << 20):
@@ -438,9 +473,12 @@ class ShardedQuery:
         if not self.exchange:  # one shard's list is final (its count is already <= k)
             rk, rv, ri, rn = topk_record_views(rec)
             return rk[:k], ri[:k], rv[:k], rn
-        return merge_topk_device(rec, k, descending, self.launch_aux, self._buf("tmk", k, torch.float32),
-                                 self._buf("tmi", k, torch.int64), self._buf("tmv", k, torch.float32),
-                                 self._buf("tmn", 1, torch.int64), self.group)
+        self._ex_mark()
+        out = merge_topk_device(rec, k, descending, self.launch_aux, self._buf("tmk", k, torch.float32),
+                                self._buf("tmi", k, torch.int64), self._buf("tmv", k, torch.float32),
+                                self._buf("tmn", 1, torch.int64), self.group)
+        self._ex_mark()
+        return out
 
     def topk(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int, descending: bool):
         """Global top-K as host tensors (topk_merged_device + one read-back)."""
