@@ -83,13 +83,17 @@ class ResidentShards {
   // combine through one RCCL all-reduce of the dense window, others by a host merge
   GroupResult group_sum(const std::string &val_cuda, const std::string &key_cuda, const std::string &cond_cuda,
                         int32_t key_lo = 0) const;
-  // ORDER BY order [DESC] LIMIT k (1..32) WHERE cond, SELECT select (empty: the
-  // order key): K candidates per shard, ONE RCCL all-gather, a merge on the host
-  TopkResult topk(const std::string &order_cuda, const std::string &cond_cuda, const std::string &select_cuda, int k,
-                  bool descending) const;
+  // ORDER BY order [DESC] LIMIT k WHERE cond, SELECT select (empty: the order
+  // key), best first, ties by row: k <= 32 K candidates per shard (wx_topk),
+  // larger k each shard's first k rows (wx_order_head); ONE RCCL all-gather of
+  // the records and the merge on the first shard's device
+  TopkResult topk(const std::string &order_cuda, const std::string &cond_cuda, const std::string &select_cuda,
+                  int64_t k, bool descending) const;
 
  private:
   ResidentShards();
+  TopkResult topk_heads(const std::string &order_cuda, const std::string &cond_cuda, const std::string &select_cuda,
+                        int64_t k, bool descending) const;
   struct Impl;
   std::unique_ptr<Impl> impl_;
 };

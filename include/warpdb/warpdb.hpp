@@ -55,9 +55,11 @@ class WarpDB {
   // keys on a GPU: merged on the host).  Groups in ascending key order with
   // double sums and counts: SUM / COUNT / AVG (MIN / MAX are refused).
   warpdb::GroupResult query_multi_gpu_group(const std::string &sql, int32_t key_window_lo = 0);
-  // "SELECT e FROM t [WHERE c] ORDER BY o [ASC|DESC] LIMIT k" (k <= 32) over
-  // every GPU: K candidates per GPU, one RCCL all-gather, the (key, row) merge.
-  // The winning ORDER BY keys, global row numbers and SELECT values, best first.
+  // "SELECT e FROM t [WHERE c] ORDER BY o [ASC|DESC] LIMIT k [OFFSET n]" over
+  // every GPU: per GPU its best OFFSET + LIMIT rows (top-K candidates up to 32,
+  // beyond that the sorted head), one RCCL all-gather, the (key, row) merge on
+  // the device.  The winning ORDER BY keys, global row numbers and SELECT
+  // values, best first.
   warpdb::TopkResult query_multi_gpu_topk(const std::string &sql);
   // Zero-copy result: dense device buffer as an ArrowDeviceArray (ROCm).
   void query_arrow_device(const std::string &expr, ArrowDeviceArray *out_array, ArrowSchema *out_schema);

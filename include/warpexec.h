@@ -305,6 +305,32 @@ wx_status wx_topk_merge(const wx_topk_record *d_records, int32_t n_records, int3
                         const wx_launch *launch, float *d_keys, int64_t *d_idx, float *d_vals,
                         int64_t *d_count, int64_t *h_count, char *err, size_t errlen);
 
+/* ORDER BY .. LIMIT of any length over row shards (the k > 32 form of
+ * wx_topk / wx_topk_merge; single-GPU query_sql sorts the whole projection
+ * with wx_sort_*_limit, src/warpdb.cpp:453-455,483-495).  A head record of
+ * capacity cap holds: count (int64) | keys (float x cap) | vals (float x cap)
+ * | rows (int64 x cap); WX_HEAD_RECORD_BYTES(cap) bytes, so the records of all
+ * shards are one all-gather of bytes.
+ *
+ * wx_order_head: this shard's first min(limit, passing) rows in ORDER BY
+ * order -- the rows passing cond, keyed by order_expr, stably sorted (the
+ * order of wx_sort_by_key: NaN keys last, -0.0 == +0.0, ties by ascending
+ * row), with select_expr's value (null: the key) and the global row
+ * (row_base + row) -- written to d_record (limit <= cap).  Synchronous (the
+ * sort needs the passing count).  Scratch: 16 bytes per table row.
+ *
+ * wx_head_merge: the global head of n_records shard records (record order =
+ * row order): the first min(limit, total) of their candidates in the same
+ * order, keys / rows / vals to the (nullable) outputs, the count to d_count /
+ * h_count.  n_records * cap < 2^32. */
+#define WX_HEAD_RECORD_BYTES(cap) (8 + 16 * (int64_t)(cap))
+wx_status wx_order_head(const wx_table *table, const char *order_expr, const char *cond, const char *select_expr,
+                        int64_t limit, int32_t descending, const wx_launch *launch, int64_t row_base, void *d_record,
+                        int64_t cap, char *err, size_t errlen);
+wx_status wx_head_merge(const void *d_records, int32_t n_records, int64_t cap, int64_t limit, int32_t descending,
+                        const wx_launch *launch, float *d_keys, int64_t *d_rows, float *d_vals, int64_t *d_count,
+                        int64_t *h_count, char *err, size_t errlen);
+
 /* In-place sorts used by the legacy jit_sort_* entry points.  Stable. */
 wx_status wx_sort_pairs(int32_t *d_keys, float *d_vals, int64_t count, int32_t ascending,
                         const wx_launch *launch, char *err, size_t errlen);

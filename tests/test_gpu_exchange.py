@@ -472,3 +472,10 @@ def _warpdb_multi_against_oracle(tmp_path):
     k2, rows2, v2 = db.query_multi_gpu_topk("SELECT price FROM t ORDER BY price DESC LIMIT 7")
     ok2, oi2, ov2 = ora.topk(hs, "price", 7, True, select_expr="price")
     assert np.array_equal(rows2, oi2) and np.array_equal(bits(v2), bits(ov2))
+    # OFFSET + LIMIT beyond the 32-candidate records: the shards' sorted heads
+    # (wx_order_head), one all-gather of head records, wx_head_merge
+    k3, rows3, v3 = db.query_multi_gpu_topk(
+        "SELECT price * quantity FROM t WHERE quantity < 60 ORDER BY price ASC LIMIT 300 OFFSET 40")
+    ok3, oi3, ov3 = ora.topk(hs, "price", 340, False, cond="quantity < 60", select_expr="price * quantity")
+    assert np.array_equal(rows3, oi3[40:]) and np.array_equal(bits(k3), bits(ok3[40:]))
+    assert np.array_equal(bits(v3), bits(ov3[40:]))

@@ -1,10 +1,13 @@
 """GPU tests of GROUP BY with many distinct keys (round 3).
 
-wx_group_sum with a capacity above 4096 probes the passing rows' key range
-first: a range that fits the 2048-key LDS window moves the window onto it; a
-range up to 2^26 keys takes the range-partitioned kernels (hist -> scan ->
-scatter -> LDS aggregation -> emit, wx_template.hip wx_group_part_*); wider
-ranges keep the window + global hash.  Every form against the oracle's
+wx_group_sum with a capacity above 4096 finds the passing rows' key range
+first (the previous call's range, a sample, or an exact pass): a range that
+fits the 2048-key LDS window moves the window onto it; a range up to 2^24
+keys takes the range-partitioned kernels (tiles sorted in place by partition
++ run directory -> plan -> LDS aggregation per work item -> count -> emit,
+wx_template.hip wx_group_part_*; rows outside a guessed range send the query
+round again over the exact range); wider ranges keep the window + global
+hash.  Every form against the oracle's
 std::map-order double sums (tests/sql_features_test.cpp:14-19 intent): keys
 and counts exact, sums to 1e-12 relative (double sums of float values in a
 different order; exact whenever the bit-span bound of DESIGN.md 5.2 holds).
@@ -51,11 +54,12 @@ def _check(cols, key_expr="quantity", cond=None, **kw):
 
 
 @pytest.mark.parametrize("lo,span", [(0, 1_000_000), (-500_000, 100_000), (7, 4_097), (-(2 ** 31), 300_000),
-                                     (2 ** 31 - 200_000, 200_000), (0, 2 ** 26)])
+                                     (2 ** 31 - 200_000, 200_000), (0, 2 ** 24), (0, 2 ** 26)])
 def test_partitioned_uniform_keys(lo, span):
     i = np.arange(N, dtype=np.int64)
     keys = lo + ((i * 2654435761) % span)
-    if span == 2 ** 26:  # the widest partitioned range: its two ends present, sparse inside
+    if span >= 2 ** 24:  # its two ends present, sparse inside: 2^24 is the widest partitioned range (2048
+        # partitions), 2^26 takes the window + global hash
         keys = lo + ((i * 2654435761) % 5000) * (span // 5000)
         keys[0], keys[1] = lo, lo + span - 1
     n = _check(_table(keys))
@@ -128,3 +132,67 @@ def test_partitioned_sample_misses_outliers(guess, monkeypatch):
     cols = _table(keys)
     _check(cols)
     _check(cols, cond="price > 39.9", lowered_cond="(price[idx] > 39.9f)")
+
+
+def test_partitioned_selective_where_exact_probe():
+    """a WHERE so selective that the 65 536-row sample sees
+    no passing row sends the query through the exact min / max pass, which
+    must visit every row -- here the passing rows, and the extreme keys, sit
+    only at quad offsets 256..511 (mod 1024) that a 256-thread launch of a
+    512-thread loop once skipped.  About 1700 partitions (span ~1.4e7)."""
+    n = N
+    i = np.arange(n, dtype=np.int64)
+    keys = (i * 7919) % 300_000
+    flag = np.zeros(n, np.float32)
+    sel = ((i // 4) % 1024 >= 256) & ((i // 4) % 1024 < 512)
+    s = np.arange(65536, dtype=np.int64)
+    sampled = s * (n // 65536) + (s * (n % 65536)) // 65536  # wx_group_part_sample's rows
+    sel[sampled] = False
+    flag[sel] = 1.0
+    rows = np.flatnonzero(sel)
+    keys[rows[5]], keys[rows[len(rows) // 2]] = -5_000_000, 9_000_000
+    cols = _table(keys)
+    cols["flag"] = flag
+    m = _check(cols, cond="flag > 0", lowered_cond="(flag[idx] > 0.0f)")
+    assert m == len(np.unique(keys[sel]))
+
+
+def test_partitioned_memo_survives_rewritten_table():
+    """The key range is remembered per (expressions, columns, rows) and only
+    ever used as a guess: the same query again, then over the same buffers
+    rewritten in place with keys outside the remembered range (the pass
+    counts them and goes round again over the exact range), then with few
+    keys (the window path)."""
+    i = np.arange(N, dtype=np.int64)
+    cols = _table((i * 31) % 500_000)
+    table, tensors = dev_table(cols)
+    cap = 1 << 20
+
+    def run():
+        k = torch.empty(cap, dtype=torch.int32, device="cuda")
+        s = torch.empty(cap, dtype=torch.float64, device="cuda")
+        c = torch.empty(cap, dtype=torch.int64, device="cuda")
+        g = wx.group_sum(table, "price[idx]", "quantity[idx]", None, launch(), 0, cap, k.data_ptr(), s.data_ptr(),
+                         c.data_ptr())
+        return k[:g].cpu().numpy(), s[:g].cpu().numpy(), c[:g].cpu().numpy()
+
+    def want():
+        return ora.group_sum(ora.HostTable(cols), "price", "quantity", None, capacity=1 << 22)
+
+    for keys in ((i * 31) % 500_000, (i * 31) % 500_000, 3_000_000 + (i * 17) % 900_000, 40 + i % 700,
+                 (i * 13) % 250_000):
+        cols["quantity"] = keys.astype(np.int32)
+        tensors["quantity"].copy_(torch.from_numpy(cols["quantity"]))
+        gk, gs, gc = run()
+        rk, rs, rc = want()
+        assert np.array_equal(gk, rk) and np.array_equal(gc, rc)
+        np.testing.assert_allclose(gs, rs, rtol=1e-12, atol=0)
+
+
+def test_partitioned_skewed_keys():
+    """Half the rows on one key, the rest spread over 600 000 keys: one
+    partition far heavier than the others (its work items stay whole
+    workgroup ranges)."""
+    i = np.arange(N, dtype=np.int64)
+    keys = np.where(i % 2 == 0, 123_456, (i * 2654435761) % 600_000)
+    _check(_table(keys))

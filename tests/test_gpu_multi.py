@@ -199,10 +199,11 @@ def test_sharded_query_single_process_matches_oracle():
     # keys partly outside the window: the extras path
     k, sm, cn = q3.group_sum("price[idx]", "quantity[idx]", None, key_lo=300)
     assert np.array_equal(k.cpu().numpy(), rk) and np.array_equal(sm.cpu().numpy(), rsum)
-    tk, ti, tv = q2.topk("price[idx]", None, "discount(price[idx], 0.9f)", 5, True)
-    ok_, oi, ov = ora.topk(ora.HostTable(c2), "price", 5, True, select_expr="discount(price, 0.9)")
-    assert np.array_equal(ti.numpy(), oi) and np.array_equal(bits(tk.numpy()), bits(ok_))
-    assert np.array_equal(bits(tv.numpy()), bits(ov))
+    for k in (5, 700):  # 700: the sorted-head form (wx_order_head + wx_head_merge)
+        tk, ti, tv = q2.topk("price[idx]", None, "discount(price[idx], 0.9f)", k, True)
+        ok_, oi, ov = ora.topk(ora.HostTable(c2), "price", k, True, select_expr="discount(price, 0.9)")
+        assert np.array_equal(ti.numpy(), oi) and np.array_equal(bits(tk.numpy()), bits(ok_))
+        assert np.array_equal(bits(tv.numpy()), bits(ov))
 
 
 DISCOUNT = "__device__ float discount(float price, float rate) {\n    return price * rate;\n}\n"
@@ -230,7 +231,7 @@ def test_resident_shards_synthetic_sum_and_group(devices):
         assert np.array_equal(k, rk) and np.array_equal(cn, rcnt)
         np.testing.assert_allclose(sm, rsum, rtol=1e-12, atol=0)
     # ORDER BY .. LIMIT k: K candidates per shard, one all-gather, the merge
-    for k, desc in ((5, True), (32, False), (1, True)):
+    for k, desc in ((5, True), (32, False), (1, True), (33, True), (1500, False)):  # > 32: sorted heads
         tk, ti, tv = rs_.topk("price[idx]", "(quantity[idx] < 700)", "(price[idx] * 0.9f)", k, desc)
         ok_, oi, ov = ora.topk(ora.HostTable(host), "price", k, desc, cond="quantity < 700", select_expr="price * 0.9")
         assert np.array_equal(ti, oi) and np.array_equal(bits(tk), bits(ok_)) and np.array_equal(bits(tv), bits(ov))
@@ -253,8 +254,9 @@ def test_warpdb_multi_gpu_group_and_shared_table():
     assert v.tolist() == [30.0, 20.0] and rows.tolist() == [3, 1] and k.tolist() == [30.0, 20.0]
     k, rows, v = db.query_multi_gpu_topk("SELECT price * quantity FROM test ORDER BY price DESC LIMIT 2 OFFSET 1")
     assert k.tolist() == [20.0, 15.25] and rows.tolist() == [1, 2] and v.tolist() == [80.0, 30.5]
-    with pytest.raises(RuntimeError):
-        db.query_multi_gpu_topk("SELECT price FROM test ORDER BY price DESC LIMIT 40")
+    # beyond the 32-candidate records (the sorted heads); LIMIT past the table's rows returns every row
+    k, rows, v = db.query_multi_gpu_topk("SELECT price FROM test ORDER BY price DESC LIMIT 40")
+    assert v.tolist() == [30.0, 20.0, 15.25, 10.5] and rows.tolist() == [3, 1, 2, 0]
 
 
 @pytest.mark.parametrize("rows", [3, 1000])
@@ -277,11 +279,13 @@ def test_warpdb_multi_gpu_topk_ties_nan_signed_zero(rows, tmp_path):
     db = pw.WarpDB(str(path))
     host = {"price": price, "quantity": qty}
     for desc in (True, False):
-        sql = f"SELECT price * quantity FROM t WHERE quantity > 0 ORDER BY price {'DESC' if desc else 'ASC'} LIMIT 32"
-        k, r, v = db.query_multi_gpu_topk(sql)
-        ok_, oi, ov = ora.topk(ora.HostTable(host), "price", 32, desc, cond="quantity > 0",
-                               select_expr="price * quantity")
-        assert np.array_equal(r, oi) and np.array_equal(bits(k), bits(ok_)) and np.array_equal(bits(v), bits(ov))
+        for lim in (32, 45):  # 45: the sorted heads (radix order: NaN last, -0.0 == +0.0, stable)
+            sql = (f"SELECT price * quantity FROM t WHERE quantity > 0 ORDER BY price {'DESC' if desc else 'ASC'} "
+                   f"LIMIT {lim}")
+            k, r, v = db.query_multi_gpu_topk(sql)
+            ok_, oi, ov = ora.topk(ora.HostTable(host), "price", lim, desc, cond="quantity > 0",
+                                   select_expr="price * quantity")
+            assert np.array_equal(r, oi) and np.array_equal(bits(k), bits(ok_)) and np.array_equal(bits(v), bits(ov))
 
 
 def test_two_threads_share_one_warpdb():
@@ -373,7 +377,7 @@ def test_virtual_shards_on_one_device(nshards, monkeypatch, tmp_path):
         rk, rsum, rcnt = ora.group_sum(ht, "price", "quantity")
         assert np.array_equal(k, rk) and np.array_equal(cn, rcnt)
         np.testing.assert_allclose(sm, rsum, rtol=1e-12, atol=0)
-    for k, desc in ((5, True), (32, False), (1, True)):
+    for k, desc in ((5, True), (32, False), (1, True), (33, False), (2000, True)):  # > 32: sorted heads
         tk, ti, tv = rs_.topk("price[idx]", "(quantity[idx] < 700)", "(price[idx] * 0.9f)", k, desc)
         ok_, oi, ov = ora.topk(ht, "price", k, desc, cond="quantity < 700", select_expr="price * 0.9")
         assert np.array_equal(ti, oi) and np.array_equal(bits(tk), bits(ok_)) and np.array_equal(bits(tv), bits(ov))
@@ -398,5 +402,8 @@ def test_virtual_shards_on_one_device(nshards, monkeypatch, tmp_path):
     k2, rows2, v2 = db.query_multi_gpu_topk("SELECT price FROM t ORDER BY price DESC LIMIT 7")
     ok2, oi2, ov2 = ora.topk(hs, "price", 7, True, select_expr="price")
     assert np.array_equal(rows2, oi2) and np.array_equal(bits(v2), bits(ov2))
+    k4, rows4, v4 = db.query_multi_gpu_topk("SELECT quantity FROM t ORDER BY price DESC LIMIT 100 OFFSET 9")
+    ok4, oi4, ov4 = ora.topk(hs, "price", 109, True, select_expr="quantity")
+    assert np.array_equal(rows4, oi4[9:]) and np.array_equal(bits(v4), bits(ov4[9:]))
     r3 = np.asarray(pw.WarpDB.query_multi_gpu_csv(str(path), "price * quantity WHERE price > 15", 1000), np.float32)
     assert np.array_equal(bits(r3), bits(r))

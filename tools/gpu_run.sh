@@ -5,6 +5,7 @@
 # stops the session on failure (set -e); steps:
 #   smoke                      __graft_entry__.smoke()
 #   suite[:PYTEST ARGS]        pytest -m gpu (--durations=25), e.g. suite:-k group
+#   pytest:NAME:FILES          pytest FILES -m gpu -v > NAME.log
 #   bench:NAME[:BENCH ARGS]    python3 bench.py ARGS > NAME.json
 #   prof:NAME[:BENCH ARGS]     the same bench under rocprofv3 --kernel-trace --stats
 #                              (NAME_kernel_stats.csv is the summary to keep)
@@ -34,6 +35,10 @@ for STEP in "$@"; do
       # shellcheck disable=SC2086
       timeout -k 10 1000 python3 -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
         --durations=25 $REST > "$O/pytest_gpu.log" 2>&1 ;;
+    pytest)
+      # shellcheck disable=SC2086
+      timeout -k 10 900 python3 -u -m pytest $ARGS -m gpu -x -v --timeout 300 --timeout-method thread \
+        --durations=15 > "$O/$NAME.log" 2>&1 ;;
     bench)
       # shellcheck disable=SC2086
       timeout -k 10 400 python3 bench.py $ARGS > "$O/$NAME.json" 2> "$O/$NAME.err" ;;

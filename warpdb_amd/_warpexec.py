@@ -75,6 +75,8 @@ EXPORTED_SYMBOLS = (
     "wx_group_combine_slots",
     "wx_group_merge_lists",
     "wx_topk_merge",
+    "wx_order_head",
+    "wx_head_merge",
     "wx_cast",
     "wx_topk",
     "wx_sort_pairs",
@@ -153,6 +155,8 @@ def load() -> ctypes.CDLL:
         "wx_group_partials_slots": [T, E, E, E, L, I32, P, I32, I32, I32, I64, P, P, P, P, pI64, E, S],
         "wx_group_combine_slots": [P, I32, I32, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_topk_merge": [P, I32, I32, I32, L, P, P, P, P, pI64, E, S],
+        "wx_order_head": [T, E, E, E, I64, I32, L, I64, P, I64, E, S],
+        "wx_head_merge": [P, I32, I64, I64, I32, L, P, P, P, P, pI64, E, S],
         "wx_group_merge_lists": [P, I32, I64, P, I32, L, I64, P, P, P, P, pI64, E, S],
         "wx_cast": [P, I32, P, I32, I64, L, E, S],
         "wx_topk": [T, E, E, E, I32, I32, L, I64, P, P, P, P, pI64, E, S],
@@ -393,6 +397,33 @@ def topk_merge(d_records: int, n_records: int, k: int, descending: bool, launch:
                            ctypes.byref(h) if want_count else None, err, len(err))
     _check(st, err)
     return h.value if want_count else None
+
+
+def head_record_bytes(cap: int) -> int:
+    """WX_HEAD_RECORD_BYTES: count i64 | keys f32[cap] | vals f32[cap] | rows i64[cap]."""
+    return 8 + 16 * cap
+
+
+def order_head(table: Table, order_expr: str, cond: Optional[str], select_expr: Optional[str], limit: int,
+               descending: bool, launch: WxLaunch, d_record: int, cap: int, row_base: int = 0) -> None:
+    """This shard's ORDER BY .. LIMIT head of any length into a head record (synchronous)."""
+    lib = load()
+    err = _err()
+    _check(lib.wx_order_head(ctypes.byref(table.c), _enc(order_expr), _enc(cond), _enc(select_expr), limit,
+                             1 if descending else 0, ctypes.byref(launch), row_base, d_record or None, cap, err,
+                             len(err)), err)
+
+
+def head_merge(d_records: int, n_records: int, cap: int, limit: int, descending: bool, launch: WxLaunch,
+               d_keys: int = 0, d_rows: int = 0, d_vals: int = 0, d_count: int = 0) -> int:
+    """The global head of n_records head records (device); returns its length."""
+    lib = load()
+    err = _err()
+    h = ctypes.c_int64(-1)
+    _check(lib.wx_head_merge(d_records or None, n_records, cap, limit, 1 if descending else 0, ctypes.byref(launch),
+                             d_keys or None, d_rows or None, d_vals or None, d_count or None, ctypes.byref(h), err,
+                             len(err)), err)
+    return h.value
 
 
 def cast(d_src: int, src_dtype: int, d_dst: int, dst_dtype: int, n: int, launch: WxLaunch) -> None:

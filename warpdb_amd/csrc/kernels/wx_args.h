@@ -159,30 +159,37 @@ struct WxGroupSlotsArgs {
 };
 
 // Range-partitioned GROUP BY for many distinct keys (wx_group_part_*): the
-// passing rows' keys span [key_lo, key_lo + span); partition p holds keys
-// [key_lo + p << shift, key_lo + (p + 1) << shift).  Rows are scattered as
-// (bin << 32 | value bits) pairs into partition-contiguous order, each
-// partition is aggregated in an LDS window of 1 << shift bins, and the dense
-// per-key results are compacted in ascending key order.
+// passing rows' keys span [key_lo, key_lo + P << shift); partition p holds
+// keys [key_lo + p << shift, key_lo + (p + 1) << shift).  Each 16 384-row
+// tile's passing rows are written back in place sorted by partition (f32
+// value + u16 bin), a directory word per (partition, tile) locates the runs,
+// each partition is aggregated in an LDS window of 1 << shift bins per work
+// item, and the items' partial windows are summed into ascending-key output.
 #define WX_GP_BLOCK 1024
 struct WxGroupPartArgs {
   const void *col[WX_MAX_COLS];
   wx_i64 n_rows;
-  wx_i64 rows_per_wg;  // hist / scatter: contiguous rows per workgroup (a multiple of 4)
-  int n_wg;            // G: hist / scatter workgroups
-  int n_part;          // P
+  wx_i64 rows_per_wg;   // minmax: contiguous rows per workgroup (a multiple of 4)
+  wx_i64 n_tiles;       // tiles: ceil(n_rows / WX_GP_TILE)
+  int tiles_per_wg;     // tiles of workgroup g: [g * tiles_per_wg, (g + 1) * tiles_per_wg)
+  int n_wg;             // G: tile workgroups
+  int n_part;           // P
   int key_lo;
   int shift;
-  wx_i64 *mm;           // [gridDim.x][3] per-workgroup (min key, max key, passing rows) of the probe
-  wx_u32 *pcount;       // [P][G] rows of partition p in workgroup g's range
-  wx_i64 *poff;         // [P][G] first pair slot of (p, g)
-  wx_u64 *pairs;        // [passing rows] (bin << 32 | value bits), partition-contiguous
-  wx_i64 *work;         // [n_work][2]: (p << 40 | whole-partition flag << 39 | len, start)
+  wx_i64 *mm;           // [gridDim.x][4] per workgroup (min key, max key, passing rows, rows outside the range)
+  wx_u32 *pcount;       // [P][G] passing rows of partition p in workgroup g's tiles
+  wx_u32 *dir;          // [P][n_tiles] run of partition p in tile t: start | length << 16
+  float *vals;          // [n_tiles * WX_GP_TILE] each tile's passing values, partition-sorted
+  unsigned short *bins; // [n_tiles * WX_GP_TILE] their bins (key - key_lo - p << shift)
+  wx_i64 *work;         // [work_cap][2]: (p << 40 | g0 << 20 | g1, 0)
   wx_i64 *n_work;
+  wx_u32 *pitem;        // [P + 1] first work item of partition p
   wx_i64 work_cap;
-  wx_i64 chunk;         // pairs per aggregation work item
-  double *dsum;         // [P << shift] dense per-key sums (zero between calls)
-  wx_u64 *dcnt;         // [P << shift] dense per-key counts (zero between calls)
+  wx_i64 chunk;         // at least this many rows per work item
+  wx_i64 target_items;  // about this many work items over all partitions
+  double *psum;         // [work_cap][1 << shift] partial window sums of each work item
+  wx_u32 *pcnt;         // [work_cap][1 << shift] partial window counts
+  wx_i64 *summary;      // [4] passing rows, rows outside the range, min key, max key (host-read)
   wx_u32 *pnz;          // [P] non-empty keys per partition
   int *out_keys;
   double *out_sums;
@@ -300,6 +307,31 @@ struct WxCastArgs {
   wx_i64 n;
   int src_dtype;  // wx_dtype numbering (0 int32, 1 int64, 2 float32, 3 float64)
   int dst_dtype;
+};
+
+// ORDER BY .. LIMIT heads of any length (wx_order_head / wx_head_merge).  A
+// head record is count i64 | keys f32[cap] | vals f32[cap] | rows i64[cap]
+// (WX_HEAD_RECORD_BYTES in warpexec.h).
+struct WxHeadArgs {
+  wx_i64 n;               // iota: elements
+  wx_u32 *idx;            // iota output; gather / emit: sorted positions (the sort's payload)
+  const float *keys;      // gather / emit: sorted keys
+  const float *vals;      // gather: SELECT values by position (null: the keys themselves)
+  const int *rows;        // gather: shard-local rows by position
+  wx_i64 row_base;
+  const wx_i64 *count;    // gather: passing rows; emit: gathered candidates (device)
+  wx_i64 limit;
+  unsigned char *record;  // gather: this shard's head record
+  float *cat_keys;        // concat: every record's keys, record-major
+  wx_u32 *cat_idx;        // concat: their record * cap + position
+  wx_i64 *cat_count;      // concat: candidates
+  const unsigned char *records;  // concat / emit: n_records head records
+  int n_records;
+  wx_i64 cap;
+  float *out_keys;
+  wx_i64 *out_rows;
+  float *out_vals;
+  wx_i64 *count_out;
 };
 
 struct WxSortPrepArgs {

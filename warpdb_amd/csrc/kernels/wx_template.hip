@@ -1523,22 +1523,32 @@ extern "C" __global__ __launch_bounds__(WX_GBLOCK) void wx_group_sum(WxGroupArgs
 // a per-workgroup LDS hash can absorb anything and the global hash pays two
 // memory-side atomics per row (9.1 ms per 1e8 rows, 1 % of the read
 // roofline).  Instead the rows are partitioned by key range so that each
-// partition fits an LDS window:
-//   probe    exact (min, max) key and passing rows, per workgroup (host reduces)
-//   hist     per workgroup (static contiguous row ranges): rows per partition
-//   scan     one workgroup: partition-major offsets + aggregation work items
-//   scatter  same row ranges: (bin, value) pairs to partition-contiguous slots
-//   agg      per work item (a chunk of one partition): LDS window of 1 << shift
-//            bins (ds_add_f64 / ds_add_u32), flushed to dense per-key arrays
-//   count / scan2 / emit   non-empty keys per partition, their prefix, and the
-//            outputs in ascending key order; the dense arrays are re-zeroed
+// partition fits an LDS window of 1 << shift bins.  Round 4 layout (no
+// counting pass, no partial-line scatter):
+//   tiles  each 16 384-row tile is counting-sorted by partition in LDS and
+//          written back IN PLACE (tile t's passing rows at [t * TILE, ...)):
+//          f32 values + u16 bins (6 B per passing row, full-line stores),
+//          plus a directory word (run start | run length << 16) per
+//          (partition, tile) and per-(workgroup, partition) totals; the
+//          passing rows' exact key range and the rows outside the planned
+//          range are counted on the way (mm)
+//   plan   one workgroup: range summary, and per partition its aggregation
+//          work items (runs of whole workgroup tile ranges, about `chunk`
+//          rows each); nothing to aggregate when some row fell outside
+//   agg    per work item: the partition's runs of its tiles gathered through
+//          the directory into an LDS window (ds_add_f64 / ds_add_u32),
+//          written as the item's partial window (plain stores, no atomics)
+//   count / scan2 / emit   non-empty keys per partition (over its items'
+//          partial windows), their prefix, and the outputs in ascending key
+//          order (the partials summed)
 #define WX_GP_UNROLL 2
 #define WX_GP_SPAN ((wx_i64)WX_GP_BLOCK * WX_GP_UNROLL)
 #define WX_GP_QUAD(u) (wx_base + (wx_i64)(u) * WX_GP_BLOCK + threadIdx.x)
 #define WX_DECL_GP(name, T, slot) T wx_u##slot[WX_GP_UNROLL][4];
 #define WX_LOAD_GP_FAST(name, T, slot) ::wx::load4_full<T>(wx_a.col[slot], wx_r0u, wx_u##slot[wx_u]);
 #define WX_LOAD_GP(name, T, slot) ::wx::load4_tail<T>(wx_a.col[slot], wx_r0u, wx_rend, wx_u##slot[wx_u]);
-// rows [RB, RE) of this workgroup (RB a multiple of 4), WX_GP_SPAN quads per step
+// rows [RB, RE) of this workgroup (RB a multiple of 4), WX_GP_SPAN quads per
+// step, WX_GP_BLOCK threads (the launch must use that block size)
 #define WX_RANGE_LOOP_BEGIN(RB, RE)                                                                 \
   const wx_i64 wx_rend = (RE);                                                                      \
   const wx_i64 wx_qe = (wx_rend + 3) >> 2, wx_qfull = wx_rend >> 2;                                 \
@@ -1567,110 +1577,62 @@ extern "C" __global__ __launch_bounds__(WX_GBLOCK) void wx_group_sum(WxGroupArgs
   }                       \
   }
 
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_part_minmax(WxGroupPartArgs wx_a) {
-  __shared__ int s_mn[WX_WAVES], s_mx[WX_WAVES];
-  __shared__ wx_u64 s_c[WX_WAVES];
-  int wx_mn = 0x7fffffff, wx_mx = (int)0x80000000;
-  wx_u64 wx_c = 0;
-  WX_STRIDE_LOOP_BEGIN
-  if (idx < wx_a.n_rows && WX_EVAL_COND()) {
-    const int wx_k = static_cast<int>(WX_KEY);
-    wx_mn = wx_k < wx_mn ? wx_k : wx_mn;
-    wx_mx = wx_k > wx_mx ? wx_k : wx_mx;
-    ++wx_c;
-  }
-  WX_STRIDE_LOOP_END
+// Block-wide (min key, max key, passing rows, outside rows) of per-thread
+// values, written by thread 0 to mm[4 * blockIdx.x ...] (WX_GP_BLOCK threads)
+__device__ __forceinline__ void wx_gp_stats_out(int mn, int mx, wx_u64 c, wx_u64 o, wx_i64 *mm) {
+  __shared__ int s_mn[WX_GP_BLOCK / 64], s_mx[WX_GP_BLOCK / 64];
+  __shared__ wx_u64 s_c[WX_GP_BLOCK / 64], s_o[WX_GP_BLOCK / 64];
 #pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const int a = __shfl_xor(wx_mn, o), b = __shfl_xor(wx_mx, o);
-    wx_mn = a < wx_mn ? a : wx_mn;
-    wx_mx = b > wx_mx ? b : wx_mx;
-    wx_c += __shfl_xor(wx_c, o);
+  for (int k = 32; k > 0; k >>= 1) {
+    const int a = __shfl_xor(mn, k), b = __shfl_xor(mx, k);
+    mn = a < mn ? a : mn;
+    mx = b > mx ? b : mx;
+    c += __shfl_xor(c, k);
+    o += __shfl_xor(o, k);
   }
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  if (lane == 0) { s_mn[wave] = wx_mn; s_mx[wave] = wx_mx; s_c[wave] = wx_c; }
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    s_mn[w] = mn; s_mx[w] = mx; s_c[w] = c; s_o[w] = o;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < WX_WAVES; ++w) {
-      wx_mn = s_mn[w] < wx_mn ? s_mn[w] : wx_mn;
-      wx_mx = s_mx[w] > wx_mx ? s_mx[w] : wx_mx;
-      wx_c += s_c[w];
+    for (int w = 1; w < WX_GP_BLOCK / 64; ++w) {
+      mn = s_mn[w] < mn ? s_mn[w] : mn;
+      mx = s_mx[w] > mx ? s_mx[w] : mx;
+      c += s_c[w];
+      o += s_o[w];
     }
-    wx_a.mm[3 * blockIdx.x] = wx_mn;
-    wx_a.mm[3 * blockIdx.x + 1] = wx_mx;
-    wx_a.mm[3 * blockIdx.x + 2] = (wx_i64)wx_c;
+    mm[4 * blockIdx.x] = mn;
+    mm[4 * blockIdx.x + 1] = mx;
+    mm[4 * blockIdx.x + 2] = (wx_i64)c;
+    mm[4 * blockIdx.x + 3] = (wx_i64)o;
   }
 }
 
-// Rows per partition of this workgroup's range.  With wx_a.mm set (the
-// first pass over a range guessed from a sample) it also records the exact
-// (min, max) key, the passing rows and the rows outside the guessed range
-// (mm[4g .. 4g+3]); the host keeps the counts only when there were none.
-extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_hist(WxGroupPartArgs wx_a) {
-  extern __shared__ wx_u32 wx_s_dyn[];
-  wx_u32 *s_h = wx_s_dyn;  // [P]
-  __shared__ int s_mn[WX_GP_BLOCK / 64], s_mx[WX_GP_BLOCK / 64];
-  __shared__ wx_u64 s_c[WX_GP_BLOCK / 64], s_o[WX_GP_BLOCK / 64];
-  for (int i = threadIdx.x; i < wx_a.n_part; i += WX_GP_BLOCK) s_h[i] = 0u;
-  __syncthreads();
-  const bool wx_guess = wx_a.mm != nullptr;
+// Exact (min, max) key and passing rows of each workgroup's contiguous row
+// range (the probe when no sample guess is usable); WX_GP_BLOCK threads.
+extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_minmax(WxGroupPartArgs wx_a) {
   int wx_mn = 0x7fffffff, wx_mx = (int)0x80000000;
-  wx_u64 wx_c = 0, wx_o = 0;
+  wx_u64 wx_c = 0;
   const wx_i64 wx_rb = (wx_i64)blockIdx.x * wx_a.rows_per_wg;
   const wx_i64 wx_re = wx_rb + wx_a.rows_per_wg < wx_a.n_rows ? wx_rb + wx_a.rows_per_wg : wx_a.n_rows;
   {
     WX_RANGE_LOOP_BEGIN(wx_rb, wx_re)
     if (idx < wx_rend && WX_EVAL_COND()) {
       const int wx_k = static_cast<int>(WX_KEY);
-      const wx_u32 wx_p = ((wx_u32)wx_k - (wx_u32)wx_a.key_lo) >> wx_a.shift;
-      if (wx_guess) {
-        wx_mn = wx_k < wx_mn ? wx_k : wx_mn;
-        wx_mx = wx_k > wx_mx ? wx_k : wx_mx;
-        ++wx_c;
-      }
-      if (wx_p < (wx_u32)wx_a.n_part && wx_k >= wx_a.key_lo) atomicAdd(&s_h[wx_p], 1u);
-      else if (wx_guess) ++wx_o;
-      else atomicOr(reinterpret_cast<unsigned int *>(&wx_a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+      wx_mn = wx_k < wx_mn ? wx_k : wx_mn;
+      wx_mx = wx_k > wx_mx ? wx_k : wx_mx;
+      ++wx_c;
     }
     WX_RANGE_LOOP_END
   }
-  if (wx_guess) {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-      const int a = __shfl_xor(wx_mn, o), b = __shfl_xor(wx_mx, o);
-      wx_mn = a < wx_mn ? a : wx_mn;
-      wx_mx = b > wx_mx ? b : wx_mx;
-      wx_c += __shfl_xor(wx_c, o);
-      wx_o += __shfl_xor(wx_o, o);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      const int w = threadIdx.x >> 6;
-      s_mn[w] = wx_mn; s_mx[w] = wx_mx; s_c[w] = wx_c; s_o[w] = wx_o;
-    }
-  }
-  __syncthreads();
-  for (int p = threadIdx.x; p < wx_a.n_part; p += WX_GP_BLOCK)
-    wx_a.pcount[(wx_i64)p * wx_a.n_wg + blockIdx.x] = s_h[p];
-  if (wx_guess && threadIdx.x == 0) {
-    for (int w = 1; w < WX_GP_BLOCK / 64; ++w) {
-      wx_mn = s_mn[w] < wx_mn ? s_mn[w] : wx_mn;
-      wx_mx = s_mx[w] > wx_mx ? s_mx[w] : wx_mx;
-      wx_c += s_c[w];
-      wx_o += s_o[w];
-    }
-    wx_a.mm[4 * blockIdx.x] = wx_mn;
-    wx_a.mm[4 * blockIdx.x + 1] = wx_mx;
-    wx_a.mm[4 * blockIdx.x + 2] = (wx_i64)wx_c;
-    wx_a.mm[4 * blockIdx.x + 3] = (wx_i64)wx_o;
-  }
+  wx_gp_stats_out(wx_mn, wx_mx, wx_c, 0ull, wx_a.mm);
 }
 
 // A strided sample of the rows (thread i: row i * n / S): the (min, max) key
 // and passing rows per workgroup, from which the host guesses the range of
-// the first pass (mm[3g .. 3g+2]).
+// the first pass (mm[4g .. 4g+2]).
 extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_sample(WxGroupPartArgs wx_a) {
-  __shared__ int s_mn[WX_GP_BLOCK / 64], s_mx[WX_GP_BLOCK / 64];
-  __shared__ wx_u64 s_c[WX_GP_BLOCK / 64];
   int wx_mn = 0x7fffffff, wx_mx = (int)0x80000000;
   wx_u64 wx_c = 0;
   const wx_i64 wx_s = (wx_i64)gridDim.x * WX_GP_BLOCK;
@@ -1685,28 +1647,7 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_sample(W
       wx_c = 1;
     }
   }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    const int a = __shfl_xor(wx_mn, o), b = __shfl_xor(wx_mx, o);
-    wx_mn = a < wx_mn ? a : wx_mn;
-    wx_mx = b > wx_mx ? b : wx_mx;
-    wx_c += __shfl_xor(wx_c, o);
-  }
-  if ((threadIdx.x & 63) == 0) {
-    const int w = threadIdx.x >> 6;
-    s_mn[w] = wx_mn; s_mx[w] = wx_mx; s_c[w] = wx_c;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int w = 1; w < WX_GP_BLOCK / 64; ++w) {
-      wx_mn = s_mn[w] < wx_mn ? s_mn[w] : wx_mn;
-      wx_mx = s_mx[w] > wx_mx ? s_mx[w] : wx_mx;
-      wx_c += s_c[w];
-    }
-    wx_a.mm[3 * blockIdx.x] = wx_mn;
-    wx_a.mm[3 * blockIdx.x + 1] = wx_mx;
-    wx_a.mm[3 * blockIdx.x + 2] = (wx_i64)wx_c;
-  }
+  wx_gp_stats_out(wx_mn, wx_mx, wx_c, 0ull, wx_a.mm);
 }
 
 // Exclusive scan of a device array of n values (one 1024-thread block, 4
@@ -1751,118 +1692,70 @@ __device__ __forceinline__ wx_i64 wx_block_scan_excl(const In *in, Out *out, wx_
   return carry;
 }
 
-extern "C" __global__ __launch_bounds__(1024) void wx_group_part_scan(WxGroupPartArgs a) {
-  __shared__ wx_i64 s_w[16];
-  __shared__ wx_i64 s_items;
-  const wx_i64 total = wx_block_scan_excl(a.pcount, a.poff, (wx_i64)a.n_part * a.n_wg, s_w);
-  __syncthreads();
-  // work items: each partition in chunks of a.chunk pairs; prefix of the
-  // per-partition chunk counts by a scan over P (<= 8 per thread)
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) s_items = 0;
-  __syncthreads();
-  for (int p0 = 0; p0 < a.n_part; p0 += 1024) {
-    const int p = p0 + tid;
-    wx_i64 st = 0, len = 0, nch = 0;
-    if (p < a.n_part) {
-      st = a.poff[(wx_i64)p * a.n_wg];
-      const wx_i64 en = p + 1 < a.n_part ? a.poff[(wx_i64)(p + 1) * a.n_wg] : total;
-      len = en - st;
-      nch = (len + a.chunk - 1) / a.chunk;
-    }
-    wx_i64 incl = nch;
+// Exclusive scan over the block (WX_GP_BLOCK threads, one value each) of
+// u32 values; s_w holds WX_GP_BLOCK / 64 words.  Returns the exclusive
+// prefix, the total in *tot.
+__device__ __forceinline__ wx_u32 wx_gp_block_excl(wx_u32 v, wx_u32 *s_w, wx_u32 *tot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  wx_u32 incl = v;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const wx_i64 t = __shfl_up(incl, o);
-      if (lane >= o) incl += t;
-    }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    wx_i64 wb = 0, tot = 0;
+  for (int o = 1; o < 64; o <<= 1) {
+    const wx_u32 t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  wx_u32 wb = 0, tt = 0;
 #pragma unroll
-    for (int w = 0; w < 16; ++w) {
-      const wx_i64 x = s_w[w];
-      wb += w < wave ? x : 0;
-      tot += x;
-    }
-    wx_i64 item = s_items + wb + incl - nch;
-    for (wx_i64 c = 0; c < nch; ++c, ++item) {
-      const wx_i64 cs = st + c * a.chunk;
-      const wx_i64 cl = (len - c * a.chunk) < a.chunk ? (len - c * a.chunk) : a.chunk;
-      if (item < a.work_cap) {
-        a.work[2 * item] = ((wx_i64)p << 40) | ((nch == 1 ? 1ll : 0ll) << 39) | cl;
-        a.work[2 * item + 1] = cs;
-      }
-    }
-    __syncthreads();
-    if (tid == 0) s_items += tot;
-    __syncthreads();
+  for (int w = 0; w < WX_GP_BLOCK / 64; ++w) {
+    const wx_u32 x = s_w[w];
+    wb += w < wave ? x : 0u;
+    tt += x;
   }
-  if (tid == 0) {
-    *a.n_work = s_items < a.work_cap ? s_items : a.work_cap;
-    if (s_items > a.work_cap) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
-  }
+  *tot = tt;
+  return wb + incl - v;
 }
 
-extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_scatter(WxGroupPartArgs wx_a) {
-  extern __shared__ wx_u32 wx_s_dyn[];
-  wx_i64 *s_base = reinterpret_cast<wx_i64 *>(wx_s_dyn);        // [P]
-  wx_u32 *s_cur = reinterpret_cast<wx_u32 *>(s_base + wx_a.n_part);  // [P]
-  for (int p = threadIdx.x; p < wx_a.n_part; p += WX_GP_BLOCK) {
-    s_base[p] = wx_a.poff[(wx_i64)p * wx_a.n_wg + blockIdx.x];
-    s_cur[p] = 0u;
-  }
-  __syncthreads();
-  const wx_i64 wx_rb = (wx_i64)blockIdx.x * wx_a.rows_per_wg;
-  const wx_i64 wx_re = wx_rb + wx_a.rows_per_wg < wx_a.n_rows ? wx_rb + wx_a.rows_per_wg : wx_a.n_rows;
-  const wx_u32 wx_bmask = (1u << wx_a.shift) - 1u;
-  {
-    WX_RANGE_LOOP_BEGIN(wx_rb, wx_re)
-    if (idx < wx_rend && WX_EVAL_COND()) {
-      const wx_u32 wx_d = (wx_u32) static_cast<int>(WX_KEY) - (wx_u32)wx_a.key_lo;
-      const wx_u32 wx_p = wx_d >> wx_a.shift;
-      const float wx_v = static_cast<float>(WX_EXPR);
-      if (wx_p < (wx_u32)wx_a.n_part) {
-        const wx_u32 r = atomicAdd(&s_cur[wx_p], 1u);
-        wx_a.pairs[s_base[wx_p] + r] = ((wx_u64)(wx_d & wx_bmask) << 32) | __float_as_uint(wx_v);
-      }
-    }
-    WX_RANGE_LOOP_END
-  }
-}
-
-// Staged scatter (P <= WX_GP_STAGE_MAXP): each tile of WX_GP_BLOCK x 4 x
-// WX_GP_SUNROLL rows is counting-sorted by partition in LDS (ds_add_rtn
-// ranks, a block scan of the tile's per-partition counts), then written out
-// so that consecutive threads store consecutive slots of one partition's
-// run.  Software-pipelined: the next tile's column loads are issued as soon
-// as this tile's rows are evaluated, so they are in flight during the LDS
-// phases.  The direct form above stores 8 bytes per lane to P different
-// places: 1.5 TB/s at 1e9 rows; staged without the pipelining 3.0-3.4 TB/s.
-#define WX_GP_STAGE_MAXP 2048
+#define WX_GP_STAGE_MAXP 2048  // two partitions per thread in the tile scan
 #ifndef WX_GP_SUNROLL
-#define WX_GP_SUNROLL 4  // row quads per thread per staged tile (the host sizes the LDS to match)
+#define WX_GP_SUNROLL 4  // row quads per thread per tile (the host sizes the LDS and the tiles to match)
 #endif
 #define WX_GP_TILE (WX_GP_BLOCK * 4 * WX_GP_SUNROLL)
 #define WX_GP_SSPAN ((wx_i64)WX_GP_BLOCK * WX_GP_SUNROLL)
+static_assert(WX_GP_TILE <= 32768, "directory words hold 16-bit run starts and lengths");
 #define WX_DECL_GS(name, T, slot) T wx_u##slot[WX_GP_SUNROLL][4];
 #define WX_LOAD_GS(name, T, slot) ::wx::load4_tail<T>(wx_a.col[slot], wx_r0u, wx_rend, wx_u##slot[wx_u]);
-extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_scatter_lds(WxGroupPartArgs wx_a) {
+// Tiles [g * tiles_per_wg, ...) of workgroup g, software-pipelined: the next
+// tile's column loads are issued as soon as this tile's rows are evaluated,
+// so they are in flight during the LDS phases.  Per tile: count rows per
+// partition (ds_add), scan the counts (run starts), place every row in LDS at
+// its run's next slot (ds_add_rtn on the run cursor: each row keeps only its
+// 32-bit key offset and value in registers, no rank -- with the next tile's
+// loads in flight a kept rank spills), then write the tile's runs back in
+// place.  LDS: the tile's staged values (f32) and bins (u16) + 8 B per
+// partition.
+extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(WxGroupPartArgs wx_a) {
   extern __shared__ wx_u32 wx_s_dyn[];
-  wx_u64 *s_pair = reinterpret_cast<wx_u64 *>(wx_s_dyn);          // [WX_GP_TILE] (p << 45 | bin << 32 | value)
-  wx_i64 *s_gbase = reinterpret_cast<wx_i64 *>(s_pair + WX_GP_TILE);  // [P] next global slot of (p, this workgroup)
-  wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_gbase + wx_a.n_part);  // [P] this tile's rows of p
-  wx_u32 *s_start = s_cnt + wx_a.n_part;                              // [P] first LDS slot of p
+  float *s_val = reinterpret_cast<float *>(wx_s_dyn);                       // [WX_GP_TILE]
+  unsigned short *s_bin = reinterpret_cast<unsigned short *>(s_val + WX_GP_TILE);  // [WX_GP_TILE]
+  wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_bin + WX_GP_TILE);           // [P] this tile's rows of p
+  wx_u32 *s_cur = s_cnt + wx_a.n_part;                                       // [P] next LDS slot of p's run
   __shared__ wx_u32 s_w[WX_GP_BLOCK / 64];
   const int P = wx_a.n_part;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  for (int p = tid; p < P; p += WX_GP_BLOCK) {
-    s_gbase[p] = wx_a.poff[(wx_i64)p * wx_a.n_wg + blockIdx.x];
-    s_cnt[p] = 0u;
-  }
-  const wx_i64 wx_rb = (wx_i64)blockIdx.x * wx_a.rows_per_wg;
-  const wx_i64 wx_re = wx_rb + wx_a.rows_per_wg < wx_a.n_rows ? wx_rb + wx_a.rows_per_wg : wx_a.n_rows;
+  const int tid = threadIdx.x;
+  for (int p = tid; p < P; p += WX_GP_BLOCK) s_cnt[p] = 0u;
+  // thread tid owns partitions 2 tid and 2 tid + 1 in the scan: their totals here
+  wx_u32 tot0 = 0u, tot1 = 0u;
+  const int p0 = 2 * tid, p1 = 2 * tid + 1;
+  int wx_mn = 0x7fffffff, wx_mx = (int)0x80000000;
+  wx_u64 wx_c = 0, wx_o = 0;
+  const wx_i64 t_begin = (wx_i64)blockIdx.x * wx_a.tiles_per_wg;
+  wx_i64 t_end = t_begin + wx_a.tiles_per_wg;
+  t_end = t_end < wx_a.n_tiles ? t_end : wx_a.n_tiles;
+  const wx_i64 wx_rb = t_begin * WX_GP_TILE;
+  const wx_i64 wx_re = t_end * WX_GP_TILE < wx_a.n_rows ? t_end * WX_GP_TILE : wx_a.n_rows;
   const wx_u32 wx_bmask = (1u << wx_a.shift) - 1u;
+  const wx_u32 wx_span = (wx_u32)P << wx_a.shift;
   const wx_i64 wx_rend = wx_re;
   const wx_i64 wx_qe = (wx_rend + 3) >> 2, wx_qfull = wx_rend >> 2;
   WX_COLS(WX_DECL_GS)
@@ -1882,9 +1775,9 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_scatter_
   }
   WX_GS_LOAD_TILE()
   __syncthreads();
-  for (; wx_base < wx_qe; wx_base += WX_GP_SSPAN) {
-    wx_u64 wx_pr[WX_GP_SUNROLL][4];
-    wx_u32 wx_rk[WX_GP_SUNROLL][4];
+  for (wx_i64 t = t_begin; t < t_end; ++t, wx_base += WX_GP_SSPAN) {
+    wx_u32 wx_d[WX_GP_SUNROLL][4];  // key - key_lo, or >= P << shift: not staged (failed WHERE / outside)
+    wx_u32 wx_v[WX_GP_SUNROLL][4];
 #pragma unroll
     for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u) {
       const wx_i64 wx_r0 = WX_GP_QUAD(wx_u) << 2;
@@ -1892,18 +1785,28 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_scatter_
       for (int wx_e = 0; wx_e < 4; ++wx_e) {
         WX_COLS(WX_BIND_U)
         const wx_i64 idx = wx_r0 + wx_e;
-        wx_pr[wx_u][wx_e] = ~0ull;
+        wx_d[wx_u][wx_e] = 0xffffffffu;
+        wx_v[wx_u][wx_e] = 0u;
         if (idx < wx_rend && WX_EVAL_COND()) {
-          const wx_u32 wx_d = (wx_u32) static_cast<int>(WX_KEY) - (wx_u32)wx_a.key_lo;
-          const wx_u32 wx_p = wx_d >> wx_a.shift;
-          const float wx_v = static_cast<float>(WX_EXPR);
-          if (wx_p < (wx_u32)P) {
-            wx_pr[wx_u][wx_e] = ((wx_u64)wx_p << 45) | ((wx_u64)(wx_d & wx_bmask) << 32) | __float_as_uint(wx_v);
-            wx_rk[wx_u][wx_e] = atomicAdd(&s_cnt[wx_p], 1u);
+          const int wx_k = static_cast<int>(WX_KEY);
+          const wx_u32 wx_dd = (wx_u32)wx_k - (wx_u32)wx_a.key_lo;
+          wx_mn = wx_k < wx_mn ? wx_k : wx_mn;
+          wx_mx = wx_k > wx_mx ? wx_k : wx_mx;
+          ++wx_c;
+          // keys below key_lo wrap to huge offsets: outside like keys above the range
+          if (wx_dd < wx_span) {
+            wx_d[wx_u][wx_e] = wx_dd;
+            wx_v[wx_u][wx_e] = __float_as_uint(static_cast<float>(WX_EXPR));
+            atomicAdd(&s_cnt[wx_dd >> wx_a.shift], 1u);
+          } else {
+            ++wx_o;
           }
         }
       }
     }
+    // keep the next tile's loads below this tile's evaluation (hoisted above
+    // it, both register sets are live at once and the kernel spills)
+    __builtin_amdgcn_sched_barrier(0);
     {  // the next tile's loads, in flight during this tile's LDS phases
       const wx_i64 wx_cur = wx_base;
       wx_base += WX_GP_SSPAN;
@@ -1911,121 +1814,270 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_scatter_
       wx_base = wx_cur;
     }
     __syncthreads();
-    // exclusive scan of the tile's per-partition counts (P <= 2048: two per thread)
-    const wx_u32 c0 = 2 * tid < P ? s_cnt[2 * tid] : 0u, c1 = 2 * tid + 1 < P ? s_cnt[2 * tid + 1] : 0u;
-    wx_u32 incl = c0 + c1;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const wx_u32 t = __shfl_up(incl, o);
-      if (lane >= o) incl += t;
+    // exclusive scan of the tile's per-partition counts (P <= 2048: two per
+    // thread); the owner writes both directory words, the run cursors, and
+    // clears the counts
+    const wx_u32 c0 = p0 < P ? s_cnt[p0] : 0u, c1 = p1 < P ? s_cnt[p1] : 0u;
+    wx_u32 tot;
+    const wx_u32 ex = wx_gp_block_excl(c0 + c1, s_w, &tot);
+    if (p0 < P) {
+      s_cur[p0] = ex;
+      s_cnt[p0] = 0u;
+      tot0 += c0;
+      wx_a.dir[(wx_i64)p0 * wx_a.n_tiles + t] = ex | (c0 << 16);
     }
-    if (lane == 63) s_w[wave] = incl;
-    __syncthreads();
-    wx_u32 wb = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < WX_GP_BLOCK / 64; ++w) {
-      const wx_u32 x = s_w[w];
-      wb += w < wave ? x : 0u;
-      tot += x;
+    if (p1 < P) {
+      s_cur[p1] = ex + c0;
+      s_cnt[p1] = 0u;
+      tot1 += c1;
+      wx_a.dir[(wx_i64)p1 * wx_a.n_tiles + t] = (ex + c0) | (c1 << 16);
     }
-    const wx_u32 ex = wb + incl - c0 - c1;
-    if (2 * tid < P) s_start[2 * tid] = ex;
-    if (2 * tid + 1 < P) s_start[2 * tid + 1] = ex + c0;
     __syncthreads();
 #pragma unroll
     for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u)
 #pragma unroll
       for (int wx_e = 0; wx_e < 4; ++wx_e)
-        if (wx_pr[wx_u][wx_e] != ~0ull) {
-          const wx_u32 p = (wx_u32)(wx_pr[wx_u][wx_e] >> 45);
-          s_pair[s_start[p] + wx_rk[wx_u][wx_e]] = wx_pr[wx_u][wx_e];
+        if (wx_d[wx_u][wx_e] < wx_span) {
+          const wx_u32 j = atomicAdd(&s_cur[wx_d[wx_u][wx_e] >> wx_a.shift], 1u);
+          s_val[j] = __uint_as_float(wx_v[wx_u][wx_e]);
+          s_bin[j] = (unsigned short)(wx_d[wx_u][wx_e] & wx_bmask);
         }
     __syncthreads();
-    for (wx_u32 j = tid; j < tot; j += WX_GP_BLOCK) {
-      const wx_u64 e = s_pair[j];
-      const wx_u32 p = (wx_u32)(e >> 45);
-      wx_a.pairs[s_gbase[p] + (j - s_start[p])] = e & 0x00001fffffffffffull;
-    }
-    __syncthreads();
-    for (int p = tid; p < P; p += WX_GP_BLOCK) {  // owner thread: advance the runs, clear the counts
-      s_gbase[p] += s_cnt[p];
-      s_cnt[p] = 0u;
+    // the tile's passing rows in partition order, in place: four per thread
+    // (16-byte value stores, 8-byte bin stores; slots past `tot` hold junk
+    // no directory run reaches)
+    {
+      typedef float f4v __attribute__((ext_vector_type(4)));
+      typedef unsigned short s4v __attribute__((ext_vector_type(4)));
+      f4v *ov = reinterpret_cast<f4v *>(wx_a.vals + t * WX_GP_TILE);
+      s4v *ob = reinterpret_cast<s4v *>(wx_a.bins + t * WX_GP_TILE);
+      const f4v *sv = reinterpret_cast<const f4v *>(s_val);
+      const s4v *sb = reinterpret_cast<const s4v *>(s_bin);
+      for (wx_u32 q = tid; 4 * q < tot; q += WX_GP_BLOCK) {
+        __builtin_nontemporal_store(sv[q], ov + q);
+        __builtin_nontemporal_store(sb[q], ob + q);
+      }
     }
     __syncthreads();
   }
 #undef WX_GS_LOAD_TILE
+  if (p0 < P) wx_a.pcount[(wx_i64)p0 * wx_a.n_wg + blockIdx.x] = tot0;
+  if (p1 < P) wx_a.pcount[(wx_i64)p1 * wx_a.n_wg + blockIdx.x] = tot1;
+  wx_gp_stats_out(wx_mn, wx_mx, wx_c, wx_o, wx_a.mm);
 }
 
-#define WX_GP_AGG_BATCH 4
+// One 1024-thread workgroup: the range summary (passing rows, rows outside
+// the planned range, min key, max key -> summary[0..3]) and the aggregation
+// work items.  Per partition (one wave each): its workgroups' rows
+// pcount[p][g], their exclusive prefix e_g, and K = ceil(rows / chunk)
+// items, item k taking the workgroups with e_g in [k chunk, (k + 1) chunk)
+// -- [b_k, b_(k+1)) with b_k = #{g : e_g < k chunk} (possibly empty).  Item
+// words are (p << 40 | g0 << 20 | g1, rows).  When some row fell outside the
+// range there is nothing to aggregate (the host re-plans from the exact one).
+#define WX_GP_MAX_GPL 16  // workgroups per lane in the plan's wave scans (G <= 1024)
+extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPartArgs a) {
+  __shared__ wx_u32 s_w[16];
+  __shared__ wx_i64 s_r[16][4];
+  __shared__ wx_u32 s_k[WX_GP_STAGE_MAXP];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, G = a.n_wg, P = a.n_part;
+  {  // range summary over the tile workgroups (G <= 1024: one per thread)
+    wx_i64 c = 0, o = 0, mn = 0x7fffffff, mx = -0x7fffffffll - 1;
+    if (tid < G && a.mm[4 * tid + 2]) {
+      mn = a.mm[4 * tid];
+      mx = a.mm[4 * tid + 1];
+      c = a.mm[4 * tid + 2];
+      o = a.mm[4 * tid + 3];
+    }
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) {
+      const wx_i64 x = __shfl_xor(mn, k), y = __shfl_xor(mx, k);
+      mn = x < mn ? x : mn;
+      mx = y > mx ? y : mx;
+      c += __shfl_xor(c, k);
+      o += __shfl_xor(o, k);
+    }
+    if (lane == 0) { s_r[wave][0] = c; s_r[wave][1] = o; s_r[wave][2] = mn; s_r[wave][3] = mx; }
+    __syncthreads();
+    if (tid == 0) {
+      for (int w = 1; w < 16; ++w) {
+        c += s_r[w][0];
+        o += s_r[w][1];
+        mn = s_r[w][2] < mn ? s_r[w][2] : mn;
+        mx = s_r[w][3] > mx ? s_r[w][3] : mx;
+      }
+      s_r[0][0] = c; s_r[0][1] = o;
+      a.summary[0] = c; a.summary[1] = o; a.summary[2] = mn; a.summary[3] = mx;
+    }
+    __syncthreads();
+  }
+  const bool abort = s_r[0][1] != 0;
+  wx_i64 chunk = (s_r[0][0] + a.target_items - 1) / a.target_items;
+  chunk = chunk > a.chunk ? chunk : a.chunk;
+  const int gpl = (G + 63) / 64;
+  // pass 1: rows and item count per partition
+  for (int p = wave; p < P; p += 16) {
+    wx_i64 t = 0;
+    for (int i = 0; i < gpl; ++i) {
+      const int g = lane * gpl + i;
+      t += g < G ? a.pcount[(wx_i64)p * G + g] : 0u;
+    }
+#pragma unroll
+    for (int k = 32; k > 0; k >>= 1) t += __shfl_xor(t, k);
+    if (lane == 0) s_k[p] = abort || !t ? 0u : (wx_u32)((t - 1) / chunk + 1);
+  }
+  __syncthreads();
+  const int p0 = 2 * tid, p1 = 2 * tid + 1;
+  const wx_u32 n0 = p0 < P ? s_k[p0] : 0u, n1 = p1 < P ? s_k[p1] : 0u;
+  wx_u32 tot;
+  const wx_u32 ex = wx_gp_block_excl(n0 + n1, s_w, &tot);
+  __syncthreads();
+  if (p0 < P) s_k[p0] = ex;  // s_k now holds the first item of each partition
+  if (p1 < P) s_k[p1] = ex + n0;
+  const wx_u32 cap = (wx_u32)a.work_cap;
+  if (p0 < P) a.pitem[p0] = ex < cap ? ex : cap;
+  if (p1 < P) a.pitem[p1] = ex + n0 < cap ? ex + n0 : cap;
+  if (tid == 0) {
+    a.pitem[P] = tot < cap ? tot : cap;
+    *a.n_work = tot < cap ? tot : cap;
+    if (tot > cap) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+  }
+  __syncthreads();
+  if (abort) return;
+  // pass 2: the items (b_k by a wave count of e_g < k chunk)
+  for (int p = wave; p < P; p += 16) {
+    wx_i64 e[WX_GP_MAX_GPL], loc = 0;
+    for (int i = 0; i < WX_GP_MAX_GPL; ++i) {
+      const int g = lane * gpl + i;
+      const wx_i64 c = (i < gpl && g < G) ? (wx_i64)a.pcount[(wx_i64)p * G + g] : 0;
+      e[i] = loc;
+      loc += c;
+    }
+    wx_i64 incl = loc;
+#pragma unroll
+    for (int k = 1; k < 64; k <<= 1) {
+      const wx_i64 x = __shfl_up(incl, k);
+      if (lane >= k) incl += x;
+    }
+    const wx_i64 lb = incl - loc;  // rows of the lanes below
+    wx_i64 total = __shfl(incl, 63);
+    if (!total) continue;
+    const wx_i64 K = (total - 1) / chunk + 1, first = s_k[p];
+    wx_i64 bprev = 0;
+    for (wx_i64 k = 1; k <= K; ++k) {
+      wx_i64 b = G;
+      if (k < K) {
+        wx_i64 n = 0;
+        for (int i = 0; i < gpl; ++i) {
+          const int g = lane * gpl + i;
+          n += (g < G && lb + e[i] < k * chunk) ? 1 : 0;
+        }
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
+        b = n;
+      }
+      const wx_i64 item = first + k - 1;
+      if (lane == 0 && item < a.work_cap) {
+        a.work[2 * item] = ((wx_i64)p << 40) | (bprev << 20) | b;
+        a.work[2 * item + 1] = 0;
+      }
+      bprev = b;
+    }
+  }
+}
+
+// Work item blockIdx.x: its partition's runs in the tiles of workgroups
+// [g0, g1), aggregated in an LDS window of 1 << shift bins and written as
+// the item's partial window.  The directory words of the item's tiles are
+// staged in LDS; each wave then takes WX_GP_AGG_R consecutive tiles at a time
+// and walks their runs as one sequence, 64 x WX_GP_AGG_K elements per step
+// (a lane's run found by WX_GP_AGG_R - 1 compares against the wave-uniform
+// run prefix), loads first, then the LDS adds.
+#ifndef WX_GP_AGG_R
+#define WX_GP_AGG_R 8
+#endif
+#ifndef WX_GP_AGG_K
+#define WX_GP_AGG_K 8
+#endif
+#define WX_GP_DIRCH 4096  // directory words staged per round
 extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGroupPartArgs a) {
   extern __shared__ wx_u32 wx_s_dyn[];
   const int B = 1 << a.shift;
   double *s_sum = reinterpret_cast<double *>(wx_s_dyn);  // [B]
-  wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_sum + B);   // [B]
-  const wx_i64 nw = *a.n_work;
-  for (wx_i64 w = blockIdx.x; w < nw; w += gridDim.x) {
-    const wx_i64 w0 = a.work[2 * w], start = a.work[2 * w + 1];
-    const int p = (int)(w0 >> 40);
-    const bool whole = ((w0 >> 39) & 1) != 0;
-    const wx_i64 end = start + (w0 & ((1ll << 39) - 1));
-    for (int b = threadIdx.x; b < B; b += WX_GP_BLOCK) { s_sum[b] = 0.0; s_cnt[b] = 0u; }
+  wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_sum + B);  // [B]
+  wx_u32 *s_dir = s_cnt + B;                              // [WX_GP_DIRCH]
+  const wx_i64 w = blockIdx.x;
+  if (w >= *a.n_work) return;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const wx_i64 w0 = a.work[2 * w];
+  const int p = (int)(w0 >> 40);
+  const wx_i64 g0 = (w0 >> 20) & 0xfffff, g1 = w0 & 0xfffff;
+  const wx_i64 ta = g0 * a.tiles_per_wg;
+  wx_i64 tb = g1 * a.tiles_per_wg;
+  tb = tb < a.n_tiles ? tb : a.n_tiles;
+  for (int b = tid; b < B; b += WX_GP_BLOCK) { s_sum[b] = 0.0; s_cnt[b] = 0u; }
+  const wx_u32 *dir = a.dir + (wx_i64)p * a.n_tiles;
+  for (wx_i64 c0 = ta; c0 < tb; c0 += WX_GP_DIRCH) {
+    const int nt = (int)(tb - c0 < WX_GP_DIRCH ? tb - c0 : WX_GP_DIRCH);
+    for (int i = tid; i < nt; i += WX_GP_BLOCK) s_dir[i] = dir[c0 + i];
     __syncthreads();
-    // 16-byte loads (two pairs per lane) over the even-aligned middle; the
-    // odd head and tail pair, if any, by threads 0 and 1
-    const wx_i64 q0 = (start + 1) >> 1, q1 = end >> 1;
-    if (threadIdx.x < 2) {
-      const wx_i64 i = threadIdx.x == 0 ? start : (q1 << 1);
-      const bool take = threadIdx.x == 0 ? (start & 1) && start < end : (end & 1) && (q1 << 1) >= start && q1 >= q0;
-      if (take) {
-        const wx_u64 pr = a.pairs[i];
-        atomicAdd(&s_sum[(wx_u32)(pr >> 32)], (double)__uint_as_float((wx_u32)pr));
-        atomicAdd(&s_cnt[(wx_u32)(pr >> 32)], 1u);
-      }
-    }
-    typedef wx_u64 wx_u64x2 __attribute__((ext_vector_type(2)));
-    const wx_u64x2 *pv = reinterpret_cast<const wx_u64x2 *>(a.pairs);
-    for (wx_i64 j0 = q0 + threadIdx.x; j0 < q1; j0 += (wx_i64)WX_GP_BLOCK * WX_GP_AGG_BATCH) {
-      wx_u64x2 pr[WX_GP_AGG_BATCH];
+    for (int r0 = wave * WX_GP_AGG_R; r0 < nt; r0 += (WX_GP_BLOCK / 64) * WX_GP_AGG_R) {
+      wx_u32 pre[WX_GP_AGG_R + 1];
+      wx_i64 base[WX_GP_AGG_R];
+      pre[0] = 0u;
 #pragma unroll
-      for (int j = 0; j < WX_GP_AGG_BATCH; ++j) {
-        const wx_i64 q = j0 + (wx_i64)j * WX_GP_BLOCK;
-        pr[j] = q < q1 ? __builtin_nontemporal_load(pv + q) : wx_u64x2{~0ull, ~0ull};
+      for (int r = 0; r < WX_GP_AGG_R; ++r) {
+        const wx_u32 e = __builtin_amdgcn_readfirstlane(r0 + r < nt ? s_dir[r0 + r] : 0u);
+        base[r] = (c0 + r0 + r) * WX_GP_TILE + (wx_i64)(e & 0xffffu) - (wx_i64)pre[r];
+        pre[r + 1] = pre[r] + (e >> 16);
       }
+      const wx_u32 total = pre[WX_GP_AGG_R];
+      for (wx_u32 s = 0; s < total; s += 64 * WX_GP_AGG_K) {
+        float v[WX_GP_AGG_K];
+        wx_u32 bn[WX_GP_AGG_K];
 #pragma unroll
-      for (int j = 0; j < WX_GP_AGG_BATCH; ++j) {
-        if (pr[j].x == ~0ull) continue;
-        atomicAdd(&s_sum[(wx_u32)(pr[j].x >> 32)], (double)__uint_as_float((wx_u32)pr[j].x));
-        atomicAdd(&s_cnt[(wx_u32)(pr[j].x >> 32)], 1u);
-        atomicAdd(&s_sum[(wx_u32)(pr[j].y >> 32)], (double)__uint_as_float((wx_u32)pr[j].y));
-        atomicAdd(&s_cnt[(wx_u32)(pr[j].y >> 32)], 1u);
-      }
-    }
-    __syncthreads();
-    const wx_i64 g0 = (wx_i64)p << a.shift;
-    for (int b = threadIdx.x; b < B; b += WX_GP_BLOCK) {
-      const wx_u32 c = s_cnt[b];
-      if (!c) continue;
-      if (whole) {
-        a.dsum[g0 + b] = s_sum[b];
-        a.dcnt[g0 + b] = c;
-      } else {
-        atomicAdd(&a.dsum[g0 + b], s_sum[b]);
-        atomicAdd(&a.dcnt[g0 + b], (wx_u64)c);
+        for (int k = 0; k < WX_GP_AGG_K; ++k) {
+          const wx_u32 j = s + 64 * k + lane;
+          bn[k] = 0xffffffffu;
+          if (j < total) {
+            wx_i64 bs = base[0];
+#pragma unroll
+            for (int r = 1; r < WX_GP_AGG_R; ++r) bs = j >= pre[r] ? base[r] : bs;
+            v[k] = __builtin_nontemporal_load(a.vals + bs + j);
+            bn[k] = __builtin_nontemporal_load(a.bins + bs + j);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < WX_GP_AGG_K; ++k) {
+          if (bn[k] == 0xffffffffu) continue;
+          atomicAdd(&s_sum[bn[k]], (double)v[k]);
+          atomicAdd(&s_cnt[bn[k]], 1u);
+        }
       }
     }
     __syncthreads();
   }
+  double *ps = a.psum + w * B;
+  wx_u32 *pc = a.pcnt + w * B;
+  for (int b = tid; b < B; b += WX_GP_BLOCK) {
+    ps[b] = s_sum[b];
+    pc[b] = s_cnt[b];
+  }
 }
 
-// non-empty keys of partition blockIdx.x
+// non-empty keys of partition blockIdx.x (over its items' partial windows)
 extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_count(WxGroupPartArgs a) {
   __shared__ wx_u32 s_n;
   if (threadIdx.x == 0) s_n = 0u;
   __syncthreads();
   const int B = 1 << a.shift;
-  const wx_i64 g0 = (wx_i64)blockIdx.x << a.shift;
+  const wx_i64 i0 = a.pitem[blockIdx.x], i1 = a.pitem[blockIdx.x + 1];
   wx_u32 n = 0;
-  for (int b = threadIdx.x; b < B; b += WX_GP_BLOCK) n += a.dcnt[g0 + b] != 0ull ? 1u : 0u;
+  for (int b = threadIdx.x; b < B; b += WX_GP_BLOCK) {
+    wx_u32 nz = 0;
+    for (wx_i64 i = i0; i < i1 && !nz; ++i) nz = a.pcnt[i * B + b];
+    n += nz ? 1u : 0u;
+  }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) n += __shfl_xor(n, o);
   if ((threadIdx.x & 63) == 0) atomicAdd(&s_n, n);
@@ -2043,18 +2095,26 @@ extern "C" __global__ __launch_bounds__(1024) void wx_group_part_scan2(WxGroupPa
   }
 }
 
-// partition blockIdx.x's groups at their ascending-key positions; dense arrays re-zeroed
+// partition blockIdx.x's groups at their ascending-key positions, its items'
+// partial windows summed
 extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_emit(WxGroupPartArgs a) {
   __shared__ wx_u32 s_w[WX_GP_BLOCK / 64];
   const int B = 1 << a.shift;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const wx_i64 g0 = (wx_i64)blockIdx.x << a.shift;
+  const wx_i64 i0 = a.pitem[blockIdx.x], i1 = a.pitem[blockIdx.x + 1];
+  if (i0 == i1) return;  // no rows in this partition (uniform)
   wx_i64 pos = a.pnz[blockIdx.x];
   for (int b0 = 0; b0 < B; b0 += WX_GP_BLOCK) {
     const int b = b0 + tid;
-    const wx_u64 c = b < B ? a.dcnt[g0 + b] : 0ull;
-    const wx_u32 f = c ? 1u : 0u;
-    const wx_u64 m = __builtin_amdgcn_ballot_w64(f != 0u);
+    wx_u64 c = 0;
+    double s = 0.0;
+    if (b < B)
+      for (wx_i64 i = i0; i < i1; ++i) {
+        c += a.pcnt[i * B + b];
+        s += a.psum[i * B + b];
+      }
+    const wx_u64 m = __builtin_amdgcn_ballot_w64(c != 0ull);
     if (lane == 0) s_w[wave] = (wx_u32)__builtin_popcountll(m);
     __syncthreads();
     wx_u32 wb = 0, tot = 0;
@@ -2068,11 +2128,9 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_emit(WxG
       const wx_i64 o = pos + wb + ::wx::lanes_below(m);
       if (o < a.capacity) {
         a.out_keys[o] = (int)((wx_u32)a.key_lo + (wx_u32)(g0 + b));
-        a.out_sums[o] = a.dsum[g0 + b];
+        a.out_sums[o] = s;
         a.out_counts[o] = (wx_i64)c;
       }
-      a.dsum[g0 + b] = 0.0;
-      a.dcnt[g0 + b] = 0ull;
     }
     pos += tot;
     __syncthreads();
@@ -3182,6 +3240,72 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
     case 2: wx_cast_to<float>(a); break;
     default: wx_cast_to<double>(a); break;
   }
+}
+
+// ORDER BY .. LIMIT heads of any length (the k > 32 form of the top-K
+// record, wx_order_head / wx_head_merge in warpexec.cpp): positions to carry
+// through the stable key sort, then the sorted head gathered into a record;
+// across shards the records' candidates concatenated in record order, sorted
+// the same way, and the global head emitted.
+#define WX_HEAD_KEYS(rec) reinterpret_cast<const float *>((rec) + 8)
+#define WX_HEAD_VALS(rec, cap) reinterpret_cast<const float *>((rec) + 8 + 4 * (cap))
+#define WX_HEAD_ROWS(rec, cap) reinterpret_cast<const wx_i64 *>((rec) + 8 + 8 * (cap))
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_iota(WxHeadArgs a) {
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.n; i += (wx_i64)gridDim.x * WX_BLOCK)
+    a.idx[i] = (wx_u32)i;
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_head_gather(WxHeadArgs a) {
+  const wx_i64 c = *a.count, m = c < a.limit ? c : a.limit;
+  float *k = reinterpret_cast<float *>(a.record + 8);
+  float *v = k + a.cap;
+  wx_i64 *r = reinterpret_cast<wx_i64 *>(a.record + 8 + 8 * a.cap);
+  for (wx_i64 j = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; j < m; j += (wx_i64)gridDim.x * WX_BLOCK) {
+    const wx_u32 p = a.idx[j];
+    k[j] = a.keys[j];
+    v[j] = a.vals ? a.vals[p] : a.keys[j];
+    r[j] = a.row_base + (wx_i64)a.rows[p];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<wx_i64 *>(a.record) = m;
+}
+
+// one workgroup: the records' valid candidates, record after record
+extern "C" __global__ __launch_bounds__(1024) void wx_head_concat(WxHeadArgs a) {
+  __shared__ wx_i64 s_off[1025];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    wx_i64 o = 0;
+    for (int r = 0; r < a.n_records; ++r) {
+      s_off[r] = o;
+      wx_i64 c = *reinterpret_cast<const wx_i64 *>(a.records + (wx_i64)r * (8 + 16 * a.cap));
+      c = c < 0 ? 0 : (c > a.cap ? a.cap : c);  // a bad count reads as empty / full
+      o += c;
+    }
+    s_off[a.n_records] = o;
+    *a.cat_count = o;
+  }
+  __syncthreads();
+  for (int r = 0; r < a.n_records; ++r) {
+    const unsigned char *rec = a.records + (wx_i64)r * (8 + 16 * a.cap);
+    const wx_i64 o = s_off[r], c = s_off[r + 1] - o;
+    for (wx_i64 j = tid; j < c; j += 1024) {
+      a.cat_keys[o + j] = WX_HEAD_KEYS(rec)[j];
+      a.cat_idx[o + j] = (wx_u32)((wx_i64)r * a.cap + j);
+    }
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_head_emit(WxHeadArgs a) {
+  const wx_i64 c = *a.count, m = c < a.limit ? c : a.limit;
+  for (wx_i64 j = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; j < m; j += (wx_i64)gridDim.x * WX_BLOCK) {
+    const wx_u32 p = a.idx[j];
+    const wx_i64 r = (wx_i64)p / a.cap, q = (wx_i64)p % a.cap;
+    const unsigned char *rec = a.records + r * (8 + 16 * a.cap);
+    if (a.out_keys) a.out_keys[j] = a.keys[j];
+    if (a.out_vals) a.out_vals[j] = WX_HEAD_VALS(rec, a.cap)[q];
+    if (a.out_rows) a.out_rows[j] = WX_HEAD_ROWS(rec, a.cap)[q];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.count_out) *a.count_out = m;
 }
 
 // kind 0: float values, kind 1: int keys.  Descending order inverts the rank

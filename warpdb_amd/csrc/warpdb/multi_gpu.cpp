@@ -368,6 +368,11 @@ struct TopkScratch {
   // `out` the merged global top-K in the same layout
   DeviceBuffer cand, all, out;
   int shards = 0;
+  // k > 32: head records of capacity hcap (WX_HEAD_RECORD_BYTES), all shards'
+  // after the all-gather, and the merged head (keys f32 | rows i64 | vals f32)
+  DeviceBuffer hrec, hall, hkeys, hrows, hvals;
+  int64_t hcap = 0, hout = 0;
+  int hshards = 0;
 };
 constexpr size_t kTopkMax = 32;
 constexpr size_t kTopkRec = kTopkMax * 4 + kTopkMax * 4 + kTopkMax * 8 + 8;  // bytes per shard record
@@ -487,9 +492,105 @@ std::vector<float> ResidentShards::dense(const std::string &expr_cuda, const std
 // (global row numbers via the shard's row base) into one wx_topk_record,
 // ONE ncclAllGather of the records (bytes), then wx_topk_merge of the
 // <= 32 x shards candidates on the first shard's device.
+// ORDER BY .. LIMIT k > 32 over the shards: wx_order_head per device (this
+// shard's first k rows in ORDER BY order, global rows) into a head record of
+// capacity k, ONE ncclAllGather of the records, wx_head_merge on the first
+// shard's device (the same stable order: ties by ascending row).
+TopkResult ResidentShards::topk_heads(const std::string &order_cuda, const std::string &cond_cuda,
+                                      const std::string &select_cuda, int64_t k, bool descending) const {
+  TopkResult res;
+  const auto &ranges = impl_->ranges;
+  const size_t ns = ranges.size();
+  if (ns == 0) return res;
+  if (impl_->topk.size() < ns) impl_->topk.resize(ns);
+  const size_t rec = static_cast<size_t>(WX_HEAD_RECORD_BYTES(k));
+  std::vector<hipStream_t> streams(ns, nullptr);
+  run_per_device(ranges, [&](size_t i, const ShardRange &r) {
+    streams[i] = device_stream(r.device);
+    TopkScratch &t = impl_->topk[i];
+    if (t.hcap != k || t.hshards != static_cast<int>(ns)) {
+      t.hrec = DeviceBuffer(r.device, rec);
+      t.hall = DeviceBuffer(r.device, rec * ns);
+      t.hcap = k;
+      t.hshards = static_cast<int>(ns);
+    }
+    WxTableView v(impl_->shards[i].table);
+    wx_launch L = sync_launch(r.device, streams[i]);
+    L.flags = 0;
+    char err[8192];
+    throw_on(wx_order_head(&v.table, order_cuda.c_str(), cond_cuda.c_str(),
+                           select_cuda.empty() ? nullptr : select_cuda.c_str(), k, descending ? 1 : 0, &L, r.begin,
+                           t.hrec.ptr, k, err, sizeof(err)),
+             err);
+  });
+  bool gathered = ns > 1;
+  if (ns > 1 && !distinct_devices(ranges)) {  // co-located shards (WARPDB_VIRTUAL_SHARDS): through the host
+    std::vector<char> all(rec * ns);
+    for (size_t i = 0; i < ns; ++i) {
+      DevGuard g(ranges[i].device);
+      hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
+      hip_ok(hipMemcpy(all.data() + rec * i, impl_->topk[i].hrec.ptr, rec, hipMemcpyDeviceToHost), "hipMemcpy");
+    }
+    DevGuard g(ranges[0].device);
+    hip_ok(hipMemcpy(impl_->topk[0].hall.ptr, all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy");
+  } else if (ns > 1 || exchange_one_rank()) {
+    gathered = true;
+    Comms &cm = comms_for(static_cast<int>(ns));
+    std::lock_guard<std::mutex> clk(cm.mu);
+    if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
+    for (size_t i = 0; i < ns; ++i) {
+      DevGuard g(ranges[i].device);
+      if (ncclAllGather(impl_->topk[i].hrec.ptr, impl_->topk[i].hall.ptr, rec, ncclUint8, cm.comms[i], streams[i]) !=
+          ncclSuccess) {
+        (void)ncclGroupEnd();
+        throw std::runtime_error("ncclAllGather failed");
+      }
+    }
+    if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("RCCL all-gather failed");
+  }
+  TopkScratch &t0 = impl_->topk[0];
+  const int dev0 = ranges[0].device;
+  if (t0.hout < k) {
+    t0.hkeys = DeviceBuffer(dev0, sizeof(float) * k);
+    t0.hrows = DeviceBuffer(dev0, sizeof(int64_t) * k);
+    t0.hvals = DeviceBuffer(dev0, sizeof(float) * k);
+    t0.hout = k;
+  }
+  int64_t m = 0;
+  {
+    DevGuard dg(dev0);
+    wx_launch L = sync_launch(dev0, streams[0]);
+    L.flags = 0;
+    char err[1024];
+    throw_on(wx_head_merge(gathered ? t0.hall.ptr : t0.hrec.ptr, static_cast<int32_t>(ns), k, k, descending ? 1 : 0,
+                           &L, static_cast<float *>(t0.hkeys.ptr), static_cast<int64_t *>(t0.hrows.ptr),
+                           static_cast<float *>(t0.hvals.ptr), nullptr, &m, err, sizeof(err)),
+             err);
+    for (size_t i = 0; i < ns; ++i) {
+      DevGuard g(ranges[i].device);
+      hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
+      wx_launch Li = sync_launch(ranges[i].device, streams[i]);
+      throw_on(wx_check(&Li, err, sizeof(err)), err);
+    }
+    res.keys.resize(static_cast<size_t>(m));
+    res.rows.resize(static_cast<size_t>(m));
+    res.values.resize(static_cast<size_t>(m));
+    if (m > 0) {
+      hip_ok(hipMemcpy(res.keys.data(), t0.hkeys.ptr, sizeof(float) * m, hipMemcpyDeviceToHost), "hipMemcpy");
+      hip_ok(hipMemcpy(res.rows.data(), t0.hrows.ptr, sizeof(int64_t) * m, hipMemcpyDeviceToHost), "hipMemcpy");
+      hip_ok(hipMemcpy(res.values.data(), t0.hvals.ptr, sizeof(float) * m, hipMemcpyDeviceToHost), "hipMemcpy");
+    }
+  }
+  return res;
+}
+
 TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string &cond_cuda,
-                                const std::string &select_cuda, int k, bool descending) const {
-  if (k < 1 || k > static_cast<int>(kTopkMax)) throw std::runtime_error("top-K supports 1 <= k <= 32");
+                                const std::string &select_cuda, int64_t k, bool descending) const {
+  if (k < 1) throw std::runtime_error("top-K needs k >= 1");
+  if (k > static_cast<int64_t>(kTopkMax)) {
+    std::lock_guard<std::mutex> lk(impl_->mu);
+    return topk_heads(order_cuda, cond_cuda, select_cuda, k, descending);
+  }
   std::lock_guard<std::mutex> lk(impl_->mu);
   TopkResult res;
   const auto &ranges = impl_->ranges;
@@ -511,7 +612,7 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
     L.flags = 0;  // asynchronous until after the collective
     char err[8192];
     throw_on(wx_topk(&v.table, order_cuda.c_str(), cond_cuda.c_str(), select_cuda.empty() ? nullptr : select_cuda.c_str(),
-                     k, descending ? 1 : 0, &L, r.begin, reinterpret_cast<float *>(c),
+                     static_cast<int32_t>(k), descending ? 1 : 0, &L, r.begin, reinterpret_cast<float *>(c),
                      reinterpret_cast<int64_t *>(c + kTopkMax * 8), reinterpret_cast<float *>(c + kTopkMax * 4),
                      reinterpret_cast<int64_t *>(c + kTopkMax * 16), nullptr, err, sizeof(err)),
              err);
@@ -557,7 +658,8 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
     wx_launch L = sync_launch(dev0, streams[0]);
     L.flags = 0;
     throw_on(wx_topk_merge(static_cast<const wx_topk_record *>(gathered ? t0.all.ptr : t0.cand.ptr),
-                           static_cast<int32_t>(ns), k, descending ? 1 : 0, &L, reinterpret_cast<float *>(o),
+                           static_cast<int32_t>(ns), static_cast<int32_t>(k), descending ? 1 : 0, &L,
+                           reinterpret_cast<float *>(o),
                            reinterpret_cast<int64_t *>(o + kTopkMax * 8), reinterpret_cast<float *>(o + kTopkMax * 4),
                            reinterpret_cast<int64_t *>(o + kTopkMax * 16), nullptr, err, sizeof(err)),
              err);

@@ -264,7 +264,7 @@ PYBIND11_MODULE(pywarpdb, m) {
       .def(
           "topk",
           [](const warpdb::ResidentShards &r, const std::string &order, const std::string &cond,
-             const std::string &select, int k, bool descending) {
+             const std::string &select, int64_t k, bool descending) {
             warpdb::TopkResult t;
             {
               py::gil_scoped_release nogil;

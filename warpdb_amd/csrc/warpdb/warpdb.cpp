@@ -293,8 +293,11 @@ warpdb::TopkResult WarpDB::query_multi_gpu_topk(const std::string &sql) {
   if (dynamic_cast<const AggregationNode *>(ast.select_list[0].get()))
     throw std::runtime_error("query_multi_gpu_topk takes a plain SELECT expression");
   if (!ast.joins.empty()) throw std::runtime_error("JOIN is not supported by the execution engine");
-  const int64_t off = ast.offset ? ast.offset->count : 0, lim = ast.limit->count;
-  if (off < 0 || lim < 0 || off + lim > 32) throw std::runtime_error("query_multi_gpu_topk supports OFFSET + LIMIT <= 32");
+  const int64_t off = ast.offset ? ast.offset->count : 0;
+  int64_t lim = ast.limit->count;
+  if (off < 0 || lim < 0) throw std::runtime_error("query_multi_gpu_topk needs OFFSET, LIMIT >= 0");
+  const int64_t n_rows = static_cast<int64_t>(host_table_.num_rows());
+  if (off + lim > n_rows) lim = std::max<int64_t>(0, n_rows - off);  // nothing beyond the table
   const auto cols = names_of(host_table_);
   validate_ast(ast.select_list[0].get(), cols);
   validate_ast(ast.order_by->expr.get(), cols);
@@ -305,8 +308,8 @@ warpdb::TopkResult WarpDB::query_multi_gpu_topk(const std::string &sql) {
   }
   warpdb::TopkResult r;
   if (off + lim == 0) return r;
-  r = shards().topk(ast.order_by->expr->to_cuda_expr(), cond, ast.select_list[0]->to_cuda_expr(),
-                    static_cast<int>(off + lim), !ast.order_by->ascending);
+  r = shards().topk(ast.order_by->expr->to_cuda_expr(), cond, ast.select_list[0]->to_cuda_expr(), off + lim,
+                    !ast.order_by->ascending);
   const size_t drop = std::min(r.keys.size(), static_cast<size_t>(off));  // OFFSET
   r.keys.erase(r.keys.begin(), r.keys.begin() + drop);
   r.rows.erase(r.rows.begin(), r.rows.begin() + drop);

@@ -480,8 +480,31 @@ class ShardedQuery:
         self._ex_mark()
         return out
 
+    def topk_heads(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int,
+                   descending: bool):
+        """ORDER BY .. LIMIT k for any k (beyond the 32-candidate records):
+        this shard's first k rows in ORDER BY order (wx_order_head, global
+        rows, synchronous), ONE all-gather of the head records, wx_head_merge
+        on the device (ties by ascending row).  Returns host tensors (keys,
+        rows, vals) of the global head."""
+        wx = self.wx
+        nb = wx.head_record_bytes(k)
+        rec = self._buf("hrec", nb, torch.uint8)[:nb]
+        wx.order_head(self.table, order_expr, cond, select_expr, k, descending, self.launch_aux, rec.data_ptr(), k,
+                      row_base=self.shard.row_base)
+        allr = all_gather(rec, self.group) if self.exchange else rec
+        ok, oi, ov = (self._buf("hk", k, torch.float32), self._buf("hi", k, torch.int64),
+                      self._buf("hv", k, torch.float32))
+        m = wx.head_merge(allr.data_ptr(), allr.numel() // nb, k, k, descending, self.launch_aux, ok.data_ptr(),
+                          oi.data_ptr(), ov.data_ptr())
+        self.wx.check(self.launch)
+        return ok[:m].cpu(), oi[:m].cpu(), ov[:m].cpu()
+
     def topk(self, order_expr: str, cond: Optional[str], select_expr: Optional[str], k: int, descending: bool):
-        """Global top-K as host tensors (topk_merged_device + one read-back)."""
+        """Global top-K as host tensors (topk_merged_device + one read-back;
+        k > 32: topk_heads)."""
+        if k > TOPK_MAX:
+            return self.topk_heads(order_expr, cond, select_expr, k, descending)
         tk, ti, tv, tn = self.topk_merged_device(order_expr, cond, select_expr, k, descending)
         m = int(tn.reshape(-1)[0].item())  # synchronises
         self.wx.check(self.launch)
