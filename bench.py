@@ -559,7 +559,7 @@ def main_ranks(args):
         # LDS aggregation, emit) as one unit per step; algorithmic bytes are
         # still the 8 B/row the query reads (the roofline BASELINE prices)
         kern_avg_ms *= launches / max(1, args.steps)
-        kname = "wx_group_part_* pipeline (probe + hist + scatter + agg + emit)"
+        kname = "wx_group_part_* pipeline (sample + tiles + plan + agg + count + scan2 + emit)"
         bytes_per_launch = n * rb
     elif workload == "sort":  # histogram read + the tile passes that ran (read + write 4 B each)
         passes = max(0, round(launches / max(1, args.steps)) - 1)

@@ -595,7 +595,8 @@ def test_sort_float_plain_flip_equals_general_map(n, special, monkeypatch):
 def test_sort_ranking_modes_agree(n, monkeypatch):
     """The tiles' in-wave ranking by one LDS add per key (WARPDB_RS_LEAD=0),
     with lane 0's digit group ranked by one ballot (1, the default) and chosen
-    per pass from the histogram (auto) all give the oracle's stable order:
+    per pass from the histogram (auto), and the peer-mask ranking (the
+    non-gfx950 build) all give the oracle's stable order:
     float keys with heavy ties, and int key + row payload pairs whose keys
     skew one digit (a few small values) next to a full-range digit."""
     monkeypatch.setenv("WARPDB_SORT", "radix")
@@ -606,8 +607,12 @@ def test_sort_ranking_modes_agree(n, monkeypatch):
     for asc in (True, False):
         ref = v[np.argsort(v if asc else -v, kind="stable")]
         order = np.argsort(keys if asc else -keys.astype(np.int64), kind="stable")
-        for lead in ("0", "1", "auto"):
-            monkeypatch.setenv("WARPDB_RS_LEAD", lead)
+        # "peer": the peer-mask ranking (WX_RS_RANK_ATOMIC=0), what any target
+        # other than gfx950 builds (the atomic form's stability rests on the
+        # LDS returning same-address adds in lane order, observed on gfx950)
+        for lead in ("0", "1", "auto", "peer"):
+            monkeypatch.setenv("WARPDB_RS_RANK_ATOMIC", "0" if lead == "peer" else "")
+            monkeypatch.setenv("WARPDB_RS_LEAD", "1" if lead == "peer" else lead)
             t = torch.from_numpy(v.copy()).cuda()
             wx.sort_float(t.data_ptr(), n, asc, launch())
             assert np.array_equal(bits(t.cpu().numpy()), bits(ref)), (lead, asc)

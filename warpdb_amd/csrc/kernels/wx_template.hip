@@ -1727,26 +1727,27 @@ static_assert(WX_GP_TILE <= 32768, "directory words hold 16-bit run starts and l
 #define WX_LOAD_GS(name, T, slot) ::wx::load4_tail<T>(wx_a.col[slot], wx_r0u, wx_rend, wx_u##slot[wx_u]);
 // Tiles [g * tiles_per_wg, ...) of workgroup g, software-pipelined: the next
 // tile's column loads are issued as soon as this tile's rows are evaluated,
-// so they are in flight during the LDS phases.  Per tile: count rows per
-// partition (ds_add), scan the counts (run starts), place every row in LDS at
-// its run's next slot (ds_add_rtn on the run cursor: each row keeps only its
-// 32-bit key offset and value in registers, no rank -- with the next tile's
-// loads in flight a kept rank spills), then write the tile's runs back in
-// place.  LDS: the tile's staged values (f32) and bins (u16) + 8 B per
-// partition.
+// so they are in flight during the LDS phases, and the previous tile's
+// write-out (LDS -> HBM) opens each iteration, so its stores drain during
+// this tile's evaluation.  Per tile, three barriers: evaluate and count rows
+// per partition (ds_add); barrier; wave 0 scans the counts into run starts
+// (the directory words, the run cursors, the workgroup's per-partition
+// totals); barrier; every row placed at its run's next LDS slot (ds_add_rtn
+// on the cursor: each row keeps only its 32-bit key offset and value in
+// registers, no rank -- with the next tile's loads in flight a kept rank
+// spills); barrier.  LDS: the tile's staged values (f32) and bins (u16) +
+// 12 B per partition.
 extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(WxGroupPartArgs wx_a) {
   extern __shared__ wx_u32 wx_s_dyn[];
   float *s_val = reinterpret_cast<float *>(wx_s_dyn);                       // [WX_GP_TILE]
   unsigned short *s_bin = reinterpret_cast<unsigned short *>(s_val + WX_GP_TILE);  // [WX_GP_TILE]
   wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_bin + WX_GP_TILE);           // [P] this tile's rows of p
   wx_u32 *s_cur = s_cnt + wx_a.n_part;                                       // [P] next LDS slot of p's run
-  __shared__ wx_u32 s_w[WX_GP_BLOCK / 64];
+  wx_u32 *s_tot = s_cur + wx_a.n_part;                                       // [P] this workgroup's rows of p
+  __shared__ wx_u32 s_tile_tot;
   const int P = wx_a.n_part;
-  const int tid = threadIdx.x;
-  for (int p = tid; p < P; p += WX_GP_BLOCK) s_cnt[p] = 0u;
-  // thread tid owns partitions 2 tid and 2 tid + 1 in the scan: their totals here
-  wx_u32 tot0 = 0u, tot1 = 0u;
-  const int p0 = 2 * tid, p1 = 2 * tid + 1;
+  const int tid = threadIdx.x, lane = tid & 63;
+  for (int p = tid; p < P; p += WX_GP_BLOCK) { s_cnt[p] = 0u; s_tot[p] = 0u; }
   int wx_mn = 0x7fffffff, wx_mx = (int)0x80000000;
   wx_u64 wx_c = 0, wx_o = 0;
   const wx_i64 t_begin = (wx_i64)blockIdx.x * wx_a.tiles_per_wg;
@@ -1756,6 +1757,7 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
   const wx_i64 wx_re = t_end * WX_GP_TILE < wx_a.n_rows ? t_end * WX_GP_TILE : wx_a.n_rows;
   const wx_u32 wx_bmask = (1u << wx_a.shift) - 1u;
   const wx_u32 wx_span = (wx_u32)P << wx_a.shift;
+  const int ppl = (P + 63) / 64;  // wave 0's partitions per lane in the scan
   const wx_i64 wx_rend = wx_re;
   const wx_i64 wx_qe = (wx_rend + 3) >> 2, wx_qfull = wx_rend >> 2;
   WX_COLS(WX_DECL_GS)
@@ -1773,9 +1775,27 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
       WX_COLS(WX_LOAD_GS)                                                        \
     }                                                                            \
   }
+  // the staged tile's passing rows in partition order, written in place: four
+  // per thread (16-byte value stores, 8-byte bin stores; slots past `tot`
+  // hold junk no directory run reaches)
+#define WX_GS_WRITE_OUT(T, TOT)                                                         \
+  {                                                                                     \
+    typedef float f4v __attribute__((ext_vector_type(4)));                              \
+    typedef unsigned short s4v __attribute__((ext_vector_type(4)));                     \
+    f4v *ov = reinterpret_cast<f4v *>(wx_a.vals + (T) * WX_GP_TILE);                  \
+    s4v *ob = reinterpret_cast<s4v *>(wx_a.bins + (T) * WX_GP_TILE);                  \
+    const f4v *sv = reinterpret_cast<const f4v *>(s_val);                               \
+    const s4v *sb = reinterpret_cast<const s4v *>(s_bin);                               \
+    for (wx_u32 q = tid; 4 * q < (TOT); q += WX_GP_BLOCK) {                             \
+      __builtin_nontemporal_store(sv[q], ov + q);                                       \
+      __builtin_nontemporal_store(sb[q], ob + q);                                       \
+    }                                                                                   \
+  }
   WX_GS_LOAD_TILE()
   __syncthreads();
+  wx_u32 tot_prev = 0u;
   for (wx_i64 t = t_begin; t < t_end; ++t, wx_base += WX_GP_SSPAN) {
+    if (t > t_begin) WX_GS_WRITE_OUT(t - 1, tot_prev)
     wx_u32 wx_d[WX_GP_SUNROLL][4];  // key - key_lo, or >= P << shift: not staged (failed WHERE / outside)
     wx_u32 wx_v[WX_GP_SUNROLL][4];
 #pragma unroll
@@ -1813,26 +1833,32 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
       WX_GS_LOAD_TILE()
       wx_base = wx_cur;
     }
-    __syncthreads();
-    // exclusive scan of the tile's per-partition counts (P <= 2048: two per
-    // thread); the owner writes both directory words, the run cursors, and
-    // clears the counts
-    const wx_u32 c0 = p0 < P ? s_cnt[p0] : 0u, c1 = p1 < P ? s_cnt[p1] : 0u;
-    wx_u32 tot;
-    const wx_u32 ex = wx_gp_block_excl(c0 + c1, s_w, &tot);
-    if (p0 < P) {
-      s_cur[p0] = ex;
-      s_cnt[p0] = 0u;
-      tot0 += c0;
-      wx_a.dir[(wx_i64)p0 * wx_a.n_tiles + t] = ex | (c0 << 16);
+    __syncthreads();  // counts complete; the previous tile's write-out has read the stage
+    if (tid < 64) {
+      // wave 0: exclusive scan of the counts (lane l: partitions [l ppl, (l + 1) ppl)),
+      // the directory words and run cursors, the totals; the counts cleared
+      const int pb = lane * ppl, pe = pb + ppl < P ? pb + ppl : P;
+      wx_u32 loc = 0u;
+      for (int p = pb; p < pe; ++p) loc += s_cnt[p];
+      wx_u32 incl = loc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const wx_u32 x = __shfl_up(incl, o);
+        if (lane >= o) incl += x;
+      }
+      wx_u32 run = incl - loc;
+      for (int p = pb; p < pe; ++p) {
+        const wx_u32 c = s_cnt[p];
+        s_cur[p] = run;
+        s_cnt[p] = 0u;
+        s_tot[p] += c;
+        wx_a.dir[(wx_i64)p * wx_a.n_tiles + t] = run | (c << 16);
+        run += c;
+      }
+      if (lane == 63) s_tile_tot = incl;
     }
-    if (p1 < P) {
-      s_cur[p1] = ex + c0;
-      s_cnt[p1] = 0u;
-      tot1 += c1;
-      wx_a.dir[(wx_i64)p1 * wx_a.n_tiles + t] = (ex + c0) | (c1 << 16);
-    }
     __syncthreads();
+    tot_prev = s_tile_tot;
 #pragma unroll
     for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u)
 #pragma unroll
@@ -1843,26 +1869,11 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
           s_bin[j] = (unsigned short)(wx_d[wx_u][wx_e] & wx_bmask);
         }
     __syncthreads();
-    // the tile's passing rows in partition order, in place: four per thread
-    // (16-byte value stores, 8-byte bin stores; slots past `tot` hold junk
-    // no directory run reaches)
-    {
-      typedef float f4v __attribute__((ext_vector_type(4)));
-      typedef unsigned short s4v __attribute__((ext_vector_type(4)));
-      f4v *ov = reinterpret_cast<f4v *>(wx_a.vals + t * WX_GP_TILE);
-      s4v *ob = reinterpret_cast<s4v *>(wx_a.bins + t * WX_GP_TILE);
-      const f4v *sv = reinterpret_cast<const f4v *>(s_val);
-      const s4v *sb = reinterpret_cast<const s4v *>(s_bin);
-      for (wx_u32 q = tid; 4 * q < tot; q += WX_GP_BLOCK) {
-        __builtin_nontemporal_store(sv[q], ov + q);
-        __builtin_nontemporal_store(sb[q], ob + q);
-      }
-    }
-    __syncthreads();
   }
+  if (t_end > t_begin) WX_GS_WRITE_OUT(t_end - 1, tot_prev)
 #undef WX_GS_LOAD_TILE
-  if (p0 < P) wx_a.pcount[(wx_i64)p0 * wx_a.n_wg + blockIdx.x] = tot0;
-  if (p1 < P) wx_a.pcount[(wx_i64)p1 * wx_a.n_wg + blockIdx.x] = tot1;
+#undef WX_GS_WRITE_OUT
+  for (int p = tid; p < P; p += WX_GP_BLOCK) wx_a.pcount[(wx_i64)p * wx_a.n_wg + blockIdx.x] = s_tot[p];
   wx_gp_stats_out(wx_mn, wx_mx, wx_c, wx_o, wx_a.mm);
 }
 
@@ -1988,10 +1999,12 @@ extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPar
 // Work item blockIdx.x: its partition's runs in the tiles of workgroups
 // [g0, g1), aggregated in an LDS window of 1 << shift bins and written as
 // the item's partial window.  The directory words of the item's tiles are
-// staged in LDS; each wave then takes WX_GP_AGG_R consecutive tiles at a time
-// and walks their runs as one sequence, 64 x WX_GP_AGG_K elements per step
-// (a lane's run found by WX_GP_AGG_R - 1 compares against the wave-uniform
-// run prefix), loads first, then the LDS adds.
+// staged in LDS, WX_GP_DIRCH at a time; each wave takes groups of
+// WX_GP_AGG_R consecutive tiles and walks their runs in 64-element chunks
+// whose bounds are wave-uniform (scalar state: a lane's element is its
+// chunk's base + lane, no per-lane search), WX_GP_AGG_K chunks loaded
+// together, then added.  (A per-lane run search measured VALU-bound, 2.2 ms
+// per 1e9 rows; 16-lane groups on four runs per wave-instruction 14.5 ms.)
 #ifndef WX_GP_AGG_R
 #define WX_GP_AGG_R 8
 #endif
@@ -2022,29 +2035,38 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGr
     for (int i = tid; i < nt; i += WX_GP_BLOCK) s_dir[i] = dir[c0 + i];
     __syncthreads();
     for (int r0 = wave * WX_GP_AGG_R; r0 < nt; r0 += (WX_GP_BLOCK / 64) * WX_GP_AGG_R) {
-      wx_u32 pre[WX_GP_AGG_R + 1];
-      wx_i64 base[WX_GP_AGG_R];
-      pre[0] = 0u;
+      // the group's runs, wave-uniform: q[0] the current one, later ones behind it
+      wx_u32 q[WX_GP_AGG_R];
 #pragma unroll
-      for (int r = 0; r < WX_GP_AGG_R; ++r) {
-        const wx_u32 e = __builtin_amdgcn_readfirstlane(r0 + r < nt ? s_dir[r0 + r] : 0u);
-        base[r] = (c0 + r0 + r) * WX_GP_TILE + (wx_i64)(e & 0xffffu) - (wx_i64)pre[r];
-        pre[r + 1] = pre[r] + (e >> 16);
-      }
-      const wx_u32 total = pre[WX_GP_AGG_R];
-      for (wx_u32 s = 0; s < total; s += 64 * WX_GP_AGG_K) {
+      for (int r = 0; r < WX_GP_AGG_R; ++r) q[r] = __builtin_amdgcn_readfirstlane(r0 + r < nt ? s_dir[r0 + r] : 0u);
+      wx_i64 tcur = c0 + r0;  // the tile of q[0]
+      int left = WX_GP_AGG_R;  // runs in q (q[0] included)
+      wx_u32 off = 0;          // elements of q[0] taken
+      while (left > 0) {
+        wx_i64 addr[WX_GP_AGG_K];
+#pragma unroll
+        for (int k = 0; k < WX_GP_AGG_K; ++k) {
+          while (left > 0 && off >= (q[0] >> 16)) {  // next run (scalar)
+#pragma unroll
+            for (int r = 0; r + 1 < WX_GP_AGG_R; ++r) q[r] = q[r + 1];
+            q[WX_GP_AGG_R - 1] = 0u;
+            --left;
+            ++tcur;
+            off = 0;
+          }
+          const wx_u32 len = q[0] >> 16;
+          const wx_u32 cn = left > 0 ? (len - off < 64u ? len - off : 64u) : 0u;
+          addr[k] = (wx_u32)lane < cn ? tcur * WX_GP_TILE + (wx_i64)(q[0] & 0xffffu) + off + lane : -1;
+          off += cn;
+        }
         float v[WX_GP_AGG_K];
         wx_u32 bn[WX_GP_AGG_K];
 #pragma unroll
         for (int k = 0; k < WX_GP_AGG_K; ++k) {
-          const wx_u32 j = s + 64 * k + lane;
           bn[k] = 0xffffffffu;
-          if (j < total) {
-            wx_i64 bs = base[0];
-#pragma unroll
-            for (int r = 1; r < WX_GP_AGG_R; ++r) bs = j >= pre[r] ? base[r] : bs;
-            v[k] = __builtin_nontemporal_load(a.vals + bs + j);
-            bn[k] = __builtin_nontemporal_load(a.bins + bs + j);
+          if (addr[k] >= 0) {
+            v[k] = __builtin_nontemporal_load(a.vals + addr[k]);
+            bn[k] = __builtin_nontemporal_load(a.bins + addr[k]);
           }
         }
 #pragma unroll
