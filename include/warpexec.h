@@ -153,10 +153,15 @@ wx_status wx_reduce_stats(const wx_table *table, const char *expr, const char *c
  * Keys in [key_window_lo, key_window_lo + 2048) take the LDS fast path; at
  * most 4096 distinct keys may fall outside it unless capacity is larger.
  * With capacity > 4096 on >= 2^20 rows (a caller expecting many groups) the
- * call first finds the passing rows' key range (one host read): a range of at
- * most 2048 keys moves the window onto it, a range of up to 2^26 keys runs the
- * range-partitioned kernels, a wider one the window + hash
- * path.  Results are the same either way. */
+ * call first takes a key-range guess: the previous call's over the same
+ * expressions, columns and row count (no host read), else a 65 536-row sample
+ * (one host synchronisation), else an exact min / max pass (one more).  A
+ * range of at most 2048 keys moves the window onto it and the call stays
+ * asynchronous after that; a range of up to 2^24 keys runs the
+ * range-partitioned kernels, which end with one host read
+ * of their range summary (the call returns with the result complete, and
+ * runs again over the exact range when a row fell outside the guess); a
+ * wider one the window + hash path.  Results are the same either way. */
 wx_status wx_group_sum(const wx_table *table, const char *val_expr, const char *key_expr,
                        const char *cond, const wx_launch *launch, int32_t key_window_lo,
                        int64_t capacity, int32_t *d_keys, double *d_sums, int64_t *d_counts,

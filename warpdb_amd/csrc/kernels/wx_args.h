@@ -178,12 +178,14 @@ struct WxGroupPartArgs {
   int shift;
   wx_i64 *mm;           // [gridDim.x][4] per workgroup (min key, max key, passing rows, rows outside the range)
   wx_u32 *pcount;       // [P][G] passing rows of partition p in workgroup g's tiles
+  wx_u64 *ptotal;       // [P] passing rows of partition p (zero between calls: the plan clears it)
   wx_u32 *dir;          // [P][n_tiles] run of partition p in tile t: start | length << 16
   float *vals;          // [n_tiles * WX_GP_TILE] each tile's passing values, partition-sorted
   unsigned short *bins; // [n_tiles * WX_GP_TILE] their bins (key - key_lo - p << shift)
   wx_i64 *work;         // [work_cap][2]: (p << 40 | g0 << 20 | g1, 0)
   wx_i64 *n_work;
   wx_u32 *pitem;        // [P + 1] first work item of partition p
+  wx_u32 *order;        // [work_cap] aggregation dispatch order (items by first workgroup)
   wx_i64 work_cap;
   wx_i64 chunk;         // at least this many rows per work item
   wx_i64 target_items;  // about this many work items over all partitions

@@ -1873,7 +1873,11 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
   if (t_end > t_begin) WX_GS_WRITE_OUT(t_end - 1, tot_prev)
 #undef WX_GS_LOAD_TILE
 #undef WX_GS_WRITE_OUT
-  for (int p = tid; p < P; p += WX_GP_BLOCK) wx_a.pcount[(wx_i64)p * wx_a.n_wg + blockIdx.x] = s_tot[p];
+  for (int p = tid; p < P; p += WX_GP_BLOCK) {
+    const wx_u32 c = s_tot[p];
+    wx_a.pcount[(wx_i64)p * wx_a.n_wg + blockIdx.x] = c;
+    if (c) atomicAdd(&wx_a.ptotal[p], (wx_u64)c);
+  }
   wx_gp_stats_out(wx_mn, wx_mx, wx_c, wx_o, wx_a.mm);
 }
 
@@ -1886,11 +1890,18 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
 // words are (p << 40 | g0 << 20 | g1, rows).  When some row fell outside the
 // range there is nothing to aggregate (the host re-plans from the exact one).
 #define WX_GP_MAX_GPL 16  // workgroups per lane in the plan's wave scans (G <= 1024)
+#define WX_GP_MAX_ITEMS 4096  // work items (P + 4 x CUs + 2 <= 2048 + 1024 + 2)
+#ifndef WX_GP_AGG_ORDER
+#define WX_GP_AGG_ORDER 1  // 0: aggregation items in partition order (A/B)
+#endif
 extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPartArgs a) {
   __shared__ wx_u32 s_w[16];
   __shared__ wx_i64 s_r[16][4];
   __shared__ wx_u32 s_k[WX_GP_STAGE_MAXP];
+  __shared__ wx_u32 s_hist[1024];                 // items per first workgroup g0, then their offsets
+  __shared__ unsigned short s_ig0[WX_GP_MAX_ITEMS];  // each item's first workgroup
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, G = a.n_wg, P = a.n_part;
+  s_hist[tid] = 0u;
   {  // range summary over the tile workgroups (G <= 1024: one per thread)
     wx_i64 c = 0, o = 0, mn = 0x7fffffff, mx = -0x7fffffffll - 1;
     if (tid < G && a.mm[4 * tid + 2]) {
@@ -1925,16 +1936,12 @@ extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPar
   wx_i64 chunk = (s_r[0][0] + a.target_items - 1) / a.target_items;
   chunk = chunk > a.chunk ? chunk : a.chunk;
   const int gpl = (G + 63) / 64;
-  // pass 1: rows and item count per partition
-  for (int p = wave; p < P; p += 16) {
-    wx_i64 t = 0;
-    for (int i = 0; i < gpl; ++i) {
-      const int g = lane * gpl + i;
-      t += g < G ? a.pcount[(wx_i64)p * G + g] : 0u;
-    }
-#pragma unroll
-    for (int k = 32; k > 0; k >>= 1) t += __shfl_xor(t, k);
-    if (lane == 0) s_k[p] = abort || !t ? 0u : (wx_u32)((t - 1) / chunk + 1);
+  // pass 1: item count per partition from its rows (ptotal, summed by the
+  // tile workgroups' atomics; cleared here for the next query, aborted or not)
+  for (int p = tid; p < P; p += 1024) {
+    const wx_i64 t = (wx_i64)a.ptotal[p];
+    a.ptotal[p] = 0ull;
+    s_k[p] = abort || !t ? 0u : (wx_u32)((t - 1) / chunk + 1);
   }
   __syncthreads();
   const int p0 = 2 * tid, p1 = 2 * tid + 1;
@@ -1990,8 +1997,29 @@ extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPar
       if (lane == 0 && item < a.work_cap) {
         a.work[2 * item] = ((wx_i64)p << 40) | (bprev << 20) | b;
         a.work[2 * item + 1] = 0;
+        s_ig0[item] = (unsigned short)bprev;
+        atomicAdd(&s_hist[bprev < G ? bprev : G - 1], 1u);
       }
       bprev = b;
+    }
+  }
+  __syncthreads();
+  // pass 3: the dispatch order, by first workgroup: the items of every
+  // partition that start in the same tile range run side by side, so the
+  // aggregation reads each tile's runs (all partitions') at about the same
+  // time -- DRAM pages and L2 lines shared instead of ~1 KB random reads
+  {
+    wx_u32 tt;
+    const wx_u32 h = tid < G ? s_hist[tid] : 0u;
+    const wx_u32 ex2 = wx_gp_block_excl(h, s_w, &tt);
+    __syncthreads();
+    if (tid < G) s_hist[tid] = ex2;
+    __syncthreads();
+    const wx_i64 ni = tot < cap ? tot : cap;
+    for (wx_i64 i = tid; i < ni; i += 1024) {
+      const wx_u32 g = s_ig0[i];
+      const wx_u32 pos = atomicAdd(&s_hist[g < (wx_u32)G ? g : G - 1], 1u);
+      a.order[WX_GP_AGG_ORDER ? pos : (wx_u32)i] = (wx_u32)i;
     }
   }
 }
@@ -1999,17 +2027,23 @@ extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPar
 // Work item blockIdx.x: its partition's runs in the tiles of workgroups
 // [g0, g1), aggregated in an LDS window of 1 << shift bins and written as
 // the item's partial window.  The directory words of the item's tiles are
-// staged in LDS, WX_GP_DIRCH at a time; each wave takes groups of
-// WX_GP_AGG_R consecutive tiles and walks their runs in 64-element chunks
-// whose bounds are wave-uniform (scalar state: a lane's element is its
-// chunk's base + lane, no per-lane search), WX_GP_AGG_K chunks loaded
-// together, then added.  (A per-lane run search measured VALU-bound, 2.2 ms
-// per 1e9 rows; 16-lane groups on four runs per wave-instruction 14.5 ms.)
+// staged in LDS, WX_GP_DIRCH at a time; each wave takes WX_GP_AGG_R
+// consecutive tiles at a time and walks their runs as one sequence,
+// 64 x WX_GP_AGG_K elements per step with every lane busy: a lane finds the
+// run of its element by WX_GP_AGG_R - 1 compares against the wave-uniform run
+// prefix and selects that run's 32-bit offset from the group's first tile.
+// All loads of a step go out before its LDS adds.  Measured alternatives
+// (1e9 rows x 1e6 keys): one 64-bit select per compare 2.2 ms; wave-uniform
+// 64-row chunks (lanes idle past a run's end) 4.3 ms; 16-lane groups on four
+// runs per load instruction 14.5 ms.
 #ifndef WX_GP_AGG_R
 #define WX_GP_AGG_R 8
 #endif
 #ifndef WX_GP_AGG_K
 #define WX_GP_AGG_K 8
+#endif
+#ifndef WX_GP_AGG_DIAG_NOADD
+#define WX_GP_AGG_DIAG_NOADD 0  // diagnostic: loads without the LDS adds (results invalid)
 #endif
 #define WX_GP_DIRCH 4096  // directory words staged per round
 extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGroupPartArgs a) {
@@ -2018,8 +2052,8 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGr
   double *s_sum = reinterpret_cast<double *>(wx_s_dyn);  // [B]
   wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_sum + B);  // [B]
   wx_u32 *s_dir = s_cnt + B;                              // [WX_GP_DIRCH]
-  const wx_i64 w = blockIdx.x;
-  if (w >= *a.n_work) return;
+  if ((wx_i64)blockIdx.x >= *a.n_work) return;
+  const wx_i64 w = a.order[blockIdx.x];  // items in first-workgroup order (the plan's pass 3)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const wx_i64 w0 = a.work[2 * w];
@@ -2029,56 +2063,65 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGr
   wx_i64 tb = g1 * a.tiles_per_wg;
   tb = tb < a.n_tiles ? tb : a.n_tiles;
   for (int b = tid; b < B; b += WX_GP_BLOCK) { s_sum[b] = 0.0; s_cnt[b] = 0u; }
+#if WX_GP_AGG_DIAG_NOADD
+  float wx_diag = 0.0f;
+#endif
   const wx_u32 *dir = a.dir + (wx_i64)p * a.n_tiles;
   for (wx_i64 c0 = ta; c0 < tb; c0 += WX_GP_DIRCH) {
     const int nt = (int)(tb - c0 < WX_GP_DIRCH ? tb - c0 : WX_GP_DIRCH);
     for (int i = tid; i < nt; i += WX_GP_BLOCK) s_dir[i] = dir[c0 + i];
     __syncthreads();
     for (int r0 = wave * WX_GP_AGG_R; r0 < nt; r0 += (WX_GP_BLOCK / 64) * WX_GP_AGG_R) {
-      // the group's runs, wave-uniform: q[0] the current one, later ones behind it
-      wx_u32 q[WX_GP_AGG_R];
+      // wave-uniform: the runs' prefix pre[] and each run's start relative to
+      // the group's first tile minus its prefix (element j of the sequence in
+      // run r sits at gbase + rel[r] + j)
+      wx_u32 pre[WX_GP_AGG_R + 1];
+      int rel[WX_GP_AGG_R];
+      pre[0] = 0u;
 #pragma unroll
-      for (int r = 0; r < WX_GP_AGG_R; ++r) q[r] = __builtin_amdgcn_readfirstlane(r0 + r < nt ? s_dir[r0 + r] : 0u);
-      wx_i64 tcur = c0 + r0;  // the tile of q[0]
-      int left = WX_GP_AGG_R;  // runs in q (q[0] included)
-      wx_u32 off = 0;          // elements of q[0] taken
-      while (left > 0) {
-        wx_i64 addr[WX_GP_AGG_K];
-#pragma unroll
-        for (int k = 0; k < WX_GP_AGG_K; ++k) {
-          while (left > 0 && off >= (q[0] >> 16)) {  // next run (scalar)
-#pragma unroll
-            for (int r = 0; r + 1 < WX_GP_AGG_R; ++r) q[r] = q[r + 1];
-            q[WX_GP_AGG_R - 1] = 0u;
-            --left;
-            ++tcur;
-            off = 0;
-          }
-          const wx_u32 len = q[0] >> 16;
-          const wx_u32 cn = left > 0 ? (len - off < 64u ? len - off : 64u) : 0u;
-          addr[k] = (wx_u32)lane < cn ? tcur * WX_GP_TILE + (wx_i64)(q[0] & 0xffffu) + off + lane : -1;
-          off += cn;
-        }
+      for (int r = 0; r < WX_GP_AGG_R; ++r) {
+        const wx_u32 e = __builtin_amdgcn_readfirstlane(r0 + r < nt ? s_dir[r0 + r] : 0u);
+        rel[r] = r * WX_GP_TILE + (int)(e & 0xffffu) - (int)pre[r];
+        pre[r + 1] = pre[r] + (e >> 16);
+      }
+      const wx_i64 gbase = (c0 + r0) * WX_GP_TILE;
+      const float *gv = a.vals + gbase;
+      const unsigned short *gb = a.bins + gbase;
+      const wx_u32 total = pre[WX_GP_AGG_R];
+      for (wx_u32 s = 0; s < total; s += 64 * WX_GP_AGG_K) {
         float v[WX_GP_AGG_K];
         wx_u32 bn[WX_GP_AGG_K];
 #pragma unroll
         for (int k = 0; k < WX_GP_AGG_K; ++k) {
+          const wx_u32 j = s + 64 * k + lane;
           bn[k] = 0xffffffffu;
-          if (addr[k] >= 0) {
-            v[k] = __builtin_nontemporal_load(a.vals + addr[k]);
-            bn[k] = __builtin_nontemporal_load(a.bins + addr[k]);
+          if (j < total) {
+            int o = rel[0];
+#pragma unroll
+            for (int r = 1; r < WX_GP_AGG_R; ++r) o = j >= pre[r] ? rel[r] : o;
+            o += (int)j;
+            v[k] = __builtin_nontemporal_load(gv + o);
+            bn[k] = __builtin_nontemporal_load(gb + o);
           }
         }
 #pragma unroll
         for (int k = 0; k < WX_GP_AGG_K; ++k) {
           if (bn[k] == 0xffffffffu) continue;
+#if WX_GP_AGG_DIAG_NOADD
+          wx_diag += v[k] + (float)bn[k];
+#else
           atomicAdd(&s_sum[bn[k]], (double)v[k]);
           atomicAdd(&s_cnt[bn[k]], 1u);
+#endif
         }
       }
     }
     __syncthreads();
   }
+#if WX_GP_AGG_DIAG_NOADD
+  if (wx_diag == 1.2345f) s_cnt[0] = 1u;  // keeps the loads live
+  __syncthreads();
+#endif
   double *ps = a.psum + w * B;
   wx_u32 *pc = a.pcnt + w * B;
   for (int b = tid; b < B; b += WX_GP_BLOCK) {
