@@ -1579,9 +1579,10 @@ extern "C" __global__ __launch_bounds__(WX_GBLOCK) void wx_group_sum(WxGroupArgs
 
 // Block-wide (min key, max key, passing rows, outside rows) of per-thread
 // values, written by thread 0 to mm[4 * blockIdx.x ...] (WX_GP_BLOCK threads)
+template <int NT = WX_GP_BLOCK>
 __device__ __forceinline__ void wx_gp_stats_out(int mn, int mx, wx_u64 c, wx_u64 o, wx_i64 *mm) {
-  __shared__ int s_mn[WX_GP_BLOCK / 64], s_mx[WX_GP_BLOCK / 64];
-  __shared__ wx_u64 s_c[WX_GP_BLOCK / 64], s_o[WX_GP_BLOCK / 64];
+  __shared__ int s_mn[NT / 64], s_mx[NT / 64];
+  __shared__ wx_u64 s_c[NT / 64], s_o[NT / 64];
 #pragma unroll
   for (int k = 32; k > 0; k >>= 1) {
     const int a = __shfl_xor(mn, k), b = __shfl_xor(mx, k);
@@ -1596,7 +1597,7 @@ __device__ __forceinline__ void wx_gp_stats_out(int mn, int mx, wx_u64 c, wx_u64
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    for (int w = 1; w < WX_GP_BLOCK / 64; ++w) {
+    for (int w = 1; w < NT / 64; ++w) {
       mn = s_mn[w] < mn ? s_mn[w] : mn;
       mx = s_mx[w] > mx ? s_mx[w] : mx;
       c += s_c[w];
@@ -1720,8 +1721,16 @@ __device__ __forceinline__ wx_u32 wx_gp_block_excl(wx_u32 v, wx_u32 *s_w, wx_u32
 #ifndef WX_GP_SUNROLL
 #define WX_GP_SUNROLL 4  // row quads per thread per tile (the host sizes the LDS and the tiles to match)
 #endif
-#define WX_GP_TILE (WX_GP_BLOCK * 4 * WX_GP_SUNROLL)
-#define WX_GP_SSPAN ((wx_i64)WX_GP_BLOCK * WX_GP_SUNROLL)
+#ifndef WX_GP_TBLOCK
+// the tile kernel's workgroup: 1024 threads, one per CU, 16 384-row tiles.
+// 512 threads at two per CU (8192-row tiles) ran the tile pass 2.75 vs 2.90
+// ms per 1e9 rows x 10^6 keys but halved the runs the aggregation gathers
+// (≈ 66 rows): 2.11 vs 1.64 ms there, 4.98 vs 4.60 ms per query
+#define WX_GP_TBLOCK 1024
+#endif
+#define WX_GP_TILE (WX_GP_TBLOCK * 4 * WX_GP_SUNROLL)
+#define WX_GP_SSPAN ((wx_i64)WX_GP_TBLOCK * WX_GP_SUNROLL)
+#define WX_GT_QUAD(u) (wx_base + (wx_i64)(u) * WX_GP_TBLOCK + threadIdx.x)
 static_assert(WX_GP_TILE <= 32768, "directory words hold 16-bit run starts and lengths");
 #define WX_DECL_GS(name, T, slot) T wx_u##slot[WX_GP_SUNROLL][4];
 #define WX_LOAD_GS(name, T, slot) ::wx::load4_tail<T>(wx_a.col[slot], wx_r0u, wx_rend, wx_u##slot[wx_u]);
@@ -1737,7 +1746,7 @@ static_assert(WX_GP_TILE <= 32768, "directory words hold 16-bit run starts and l
 // registers, no rank -- with the next tile's loads in flight a kept rank
 // spills); barrier.  LDS: the tile's staged values (f32) and bins (u16) +
 // 12 B per partition.
-extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(WxGroupPartArgs wx_a) {
+extern "C" __global__ __launch_bounds__(WX_GP_TBLOCK) void wx_group_part_tiles(WxGroupPartArgs wx_a) {
   extern __shared__ wx_u32 wx_s_dyn[];
   float *s_val = reinterpret_cast<float *>(wx_s_dyn);                       // [WX_GP_TILE]
   unsigned short *s_bin = reinterpret_cast<unsigned short *>(s_val + WX_GP_TILE);  // [WX_GP_TILE]
@@ -1747,7 +1756,7 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
   __shared__ wx_u32 s_tile_tot;
   const int P = wx_a.n_part;
   const int tid = threadIdx.x, lane = tid & 63;
-  for (int p = tid; p < P; p += WX_GP_BLOCK) { s_cnt[p] = 0u; s_tot[p] = 0u; }
+  for (int p = tid; p < P; p += WX_GP_TBLOCK) { s_cnt[p] = 0u; s_tot[p] = 0u; }
   int wx_mn = 0x7fffffff, wx_mx = (int)0x80000000;
   wx_u64 wx_c = 0, wx_o = 0;
   const wx_i64 t_begin = (wx_i64)blockIdx.x * wx_a.tiles_per_wg;
@@ -1766,12 +1775,12 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
 #define WX_GS_LOAD_TILE()                                                        \
   if (WX_ALIGNED16 && wx_base + WX_GP_SSPAN <= wx_qfull) {                       \
     _Pragma("unroll") for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u) {        \
-      const wx_i64 wx_r0u = WX_GP_QUAD(wx_u) << 2;                               \
+      const wx_i64 wx_r0u = WX_GT_QUAD(wx_u) << 2;                               \
       WX_COLS(WX_LOAD_GP_FAST)                                                   \
     }                                                                            \
   } else if (wx_base < wx_qe) {                                                  \
     _Pragma("unroll") for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u) {        \
-      const wx_i64 wx_r0u = WX_GP_QUAD(wx_u) << 2;                               \
+      const wx_i64 wx_r0u = WX_GT_QUAD(wx_u) << 2;                               \
       WX_COLS(WX_LOAD_GS)                                                        \
     }                                                                            \
   }
@@ -1786,7 +1795,7 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
     s4v *ob = reinterpret_cast<s4v *>(wx_a.bins + (T) * WX_GP_TILE);                  \
     const f4v *sv = reinterpret_cast<const f4v *>(s_val);                               \
     const s4v *sb = reinterpret_cast<const s4v *>(s_bin);                               \
-    for (wx_u32 q = tid; 4 * q < (TOT); q += WX_GP_BLOCK) {                             \
+    for (wx_u32 q = tid; 4 * q < (TOT); q += WX_GP_TBLOCK) {                             \
       __builtin_nontemporal_store(sv[q], ov + q);                                       \
       __builtin_nontemporal_store(sb[q], ob + q);                                       \
     }                                                                                   \
@@ -1800,7 +1809,7 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
     wx_u32 wx_v[WX_GP_SUNROLL][4];
 #pragma unroll
     for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u) {
-      const wx_i64 wx_r0 = WX_GP_QUAD(wx_u) << 2;
+      const wx_i64 wx_r0 = WX_GT_QUAD(wx_u) << 2;
 #pragma unroll
       for (int wx_e = 0; wx_e < 4; ++wx_e) {
         WX_COLS(WX_BIND_U)
@@ -1873,12 +1882,12 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_tiles(Wx
   if (t_end > t_begin) WX_GS_WRITE_OUT(t_end - 1, tot_prev)
 #undef WX_GS_LOAD_TILE
 #undef WX_GS_WRITE_OUT
-  for (int p = tid; p < P; p += WX_GP_BLOCK) {
+  for (int p = tid; p < P; p += WX_GP_TBLOCK) {
     const wx_u32 c = s_tot[p];
     wx_a.pcount[(wx_i64)p * wx_a.n_wg + blockIdx.x] = c;
     if (c) atomicAdd(&wx_a.ptotal[p], (wx_u64)c);
   }
-  wx_gp_stats_out(wx_mn, wx_mx, wx_c, wx_o, wx_a.mm);
+  wx_gp_stats_out<WX_GP_TBLOCK>(wx_mn, wx_mx, wx_c, wx_o, wx_a.mm);
 }
 
 // One 1024-thread workgroup: the range summary (passing rows, rows outside
@@ -2032,15 +2041,17 @@ extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPar
 // 64 x WX_GP_AGG_K elements per step with every lane busy: a lane finds the
 // run of its element by WX_GP_AGG_R - 1 compares against the wave-uniform run
 // prefix and selects that run's 32-bit offset from the group's first tile.
-// All loads of a step go out before its LDS adds.  Measured alternatives
-// (1e9 rows x 1e6 keys): one 64-bit select per compare 2.2 ms; wave-uniform
-// 64-row chunks (lanes idle past a run's end) 4.3 ms; 16-lane groups on four
-// runs per load instruction 14.5 ms.
+// Measured alternatives (1e9 rows x 1e6 keys): one 64-bit select per compare
+// 2.2 ms; wave-uniform 64-row chunks (lanes idle past a run's end) 4.3 ms;
+// 16-lane groups on four runs per load instruction 14.5 ms; the dispatch
+// order by first workgroup (the plan's pass 3) took the agg from 2.3 to 1.64.
 #ifndef WX_GP_AGG_R
 #define WX_GP_AGG_R 8
 #endif
 #ifndef WX_GP_AGG_K
-#define WX_GP_AGG_K 8
+// 64-element chunks per fetch (two fetches in flight): 6 -> 4.51 ms per
+// 1e9 rows x 10^6 keys, 4 -> 4.58, 8 -> 4.65 (profiles/r04/abl_group_wide_agg.txt)
+#define WX_GP_AGG_K 6
 #endif
 #ifndef WX_GP_AGG_DIAG_NOADD
 #define WX_GP_AGG_DIAG_NOADD 0  // diagnostic: loads without the LDS adds (results invalid)
@@ -2071,51 +2082,88 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGr
     const int nt = (int)(tb - c0 < WX_GP_DIRCH ? tb - c0 : WX_GP_DIRCH);
     for (int i = tid; i < nt; i += WX_GP_BLOCK) s_dir[i] = dir[c0 + i];
     __syncthreads();
-    for (int r0 = wave * WX_GP_AGG_R; r0 < nt; r0 += (WX_GP_BLOCK / 64) * WX_GP_AGG_R) {
-      // wave-uniform: the runs' prefix pre[] and each run's start relative to
-      // the group's first tile minus its prefix (element j of the sequence in
-      // run r sits at gbase + rel[r] + j)
-      wx_u32 pre[WX_GP_AGG_R + 1];
-      int rel[WX_GP_AGG_R];
-      pre[0] = 0u;
-#pragma unroll
-      for (int r = 0; r < WX_GP_AGG_R; ++r) {
-        const wx_u32 e = __builtin_amdgcn_readfirstlane(r0 + r < nt ? s_dir[r0 + r] : 0u);
-        rel[r] = r * WX_GP_TILE + (int)(e & 0xffffu) - (int)pre[r];
-        pre[r + 1] = pre[r] + (e >> 16);
-      }
-      const wx_i64 gbase = (c0 + r0) * WX_GP_TILE;
-      const float *gv = a.vals + gbase;
-      const unsigned short *gb = a.bins + gbase;
-      const wx_u32 total = pre[WX_GP_AGG_R];
-      for (wx_u32 s = 0; s < total; s += 64 * WX_GP_AGG_K) {
-        float v[WX_GP_AGG_K];
-        wx_u32 bn[WX_GP_AGG_K];
-#pragma unroll
-        for (int k = 0; k < WX_GP_AGG_K; ++k) {
-          const wx_u32 j = s + 64 * k + lane;
-          bn[k] = 0xffffffffu;
-          if (j < total) {
-            int o = rel[0];
-#pragma unroll
-            for (int r = 1; r < WX_GP_AGG_R; ++r) o = j >= pre[r] ? rel[r] : o;
-            o += (int)j;
-            v[k] = __builtin_nontemporal_load(gv + o);
-            bn[k] = __builtin_nontemporal_load(gb + o);
-          }
-        }
-#pragma unroll
-        for (int k = 0; k < WX_GP_AGG_K; ++k) {
-          if (bn[k] == 0xffffffffu) continue;
+    // Wave-uniform walk over this wave's groups of WX_GP_AGG_R tiles (r0 =
+    // wave * R, + 16 R, ...): the runs' prefix pre[] and each run's start
+    // relative to the group's first tile minus its prefix (element j of the
+    // group's sequence in run r sits at gv + rel[r] + j).  Software-pipelined
+    // by two register sets: a step's loads are issued before the previous
+    // step's LDS adds, so 2 x 64 x WX_GP_AGG_K elements per wave are in
+    // flight; every fetch issues its loads unconditionally (junk from the
+    // array start where the walk has ended, masked out by the sentinel bin)
+    // so the adds wait only for their own set.
+    int r0 = wave * WX_GP_AGG_R - (WX_GP_BLOCK / 64) * WX_GP_AGG_R;
+    wx_u32 pre[WX_GP_AGG_R + 1];
+    int rel[WX_GP_AGG_R];
+    wx_u32 total = 0u, sj = 0u;
+    const float *gv = a.vals;
+    const unsigned short *gb = a.bins;
+#define WX_GA_NEXT_GROUP()                                                                     \
+  do {                                                                                          \
+    r0 += (WX_GP_BLOCK / 64) * WX_GP_AGG_R;                                                     \
+    total = 0u;                                                                                 \
+    sj = 0u;                                                                                    \
+    if (r0 < nt) {                                                                              \
+      pre[0] = 0u;                                                                              \
+      _Pragma("unroll") for (int r = 0; r < WX_GP_AGG_R; ++r) {                                \
+        const wx_u32 e = __builtin_amdgcn_readfirstlane(r0 + r < nt ? s_dir[r0 + r] : 0u);     \
+        rel[r] = r * WX_GP_TILE + (int)(e & 0xffffu) - (int)pre[r];                             \
+        pre[r + 1] = pre[r] + (e >> 16);                                                        \
+      }                                                                                         \
+      total = pre[WX_GP_AGG_R];                                                                 \
+      gv = a.vals + (c0 + r0) * WX_GP_TILE;                                                     \
+      gb = a.bins + (c0 + r0) * WX_GP_TILE;                                                     \
+    }                                                                                           \
+  } while (r0 < nt && total == 0u)
+    // one step's loads into (V, BN), the valid lanes' bits in OK; HAS: whether
+    // the walk had a step left
+#define WX_GA_FETCH(V, BN, OK, HAS)                                                            \
+  {                                                                                             \
+    HAS = r0 < nt;                                                                              \
+    const float *fv = HAS ? gv : a.vals;                                                        \
+    const unsigned short *fb = HAS ? gb : a.bins;                                               \
+    OK = 0u;                                                                                    \
+    _Pragma("unroll") for (int k = 0; k < WX_GP_AGG_K; ++k) {                                  \
+      const wx_u32 j = sj + 64 * k + lane;                                                      \
+      const bool ok = HAS && j < total;                                                         \
+      int o = rel[0];                                                                           \
+      _Pragma("unroll") for (int r = 1; r < WX_GP_AGG_R; ++r) o = j >= pre[r] ? rel[r] : o;    \
+      o = ok ? o + (int)j : 0;                                                                  \
+      OK |= (ok ? 1u : 0u) << k;                                                                \
+      V[k] = __builtin_nontemporal_load(fv + o);                                                \
+      BN[k] = __builtin_nontemporal_load(fb + o);                                               \
+    }                                                                                           \
+    if (HAS) {                                                                                  \
+      sj += 64 * WX_GP_AGG_K;                                                                   \
+      if (sj >= total) WX_GA_NEXT_GROUP();                                                      \
+    }                                                                                           \
+  }
 #if WX_GP_AGG_DIAG_NOADD
-          wx_diag += v[k] + (float)bn[k];
+#define WX_GA_ADD(V, BN, OK)                                                                   \
+  _Pragma("unroll") for (int k = 0; k < WX_GP_AGG_K; ++k) if ((OK >> k) & 1u) wx_diag += V[k] + (float)BN[k];
 #else
-          atomicAdd(&s_sum[bn[k]], (double)v[k]);
-          atomicAdd(&s_cnt[bn[k]], 1u);
+#define WX_GA_ADD(V, BN, OK)                                                                   \
+  _Pragma("unroll") for (int k = 0; k < WX_GP_AGG_K; ++k) {                                    \
+    if (!((OK >> k) & 1u)) continue;                                                            \
+    atomicAdd(&s_sum[BN[k]], (double)V[k]);                                                     \
+    atomicAdd(&s_cnt[BN[k]], 1u);                                                               \
+  }
 #endif
-        }
-      }
+    WX_GA_NEXT_GROUP();
+    float va[WX_GP_AGG_K], vb[WX_GP_AGG_K];
+    unsigned short ba[WX_GP_AGG_K], bb[WX_GP_AGG_K];
+    wx_u32 oka, okb;
+    bool ha, hb;
+    WX_GA_FETCH(va, ba, oka, ha)
+    while (ha) {
+      WX_GA_FETCH(vb, bb, okb, hb)
+      WX_GA_ADD(va, ba, oka)
+      if (!hb) break;
+      WX_GA_FETCH(va, ba, oka, ha)
+      WX_GA_ADD(vb, bb, okb)
     }
+#undef WX_GA_NEXT_GROUP
+#undef WX_GA_FETCH
+#undef WX_GA_ADD
     __syncthreads();
   }
 #if WX_GP_AGG_DIAG_NOADD
