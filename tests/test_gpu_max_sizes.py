@@ -138,6 +138,40 @@ def test_group_sum_past_int32_rows():
     torch.cuda.empty_cache()
 
 
+def test_group_sum_many_keys_past_int32_rows():
+    """The range-partitioned GROUP BY (10^6 keys, capacity 2^20) past 2^31
+    rows: tile indices, run directory, per-partition totals and the items'
+    tile ranges in 64-bit, against torch's bincount over the same table."""
+    n = N_BIG
+    nk = 1_000_000
+    price = torch.empty(n, dtype=torch.float32, device="cuda")
+    key = torch.empty(n, dtype=torch.int32, device="cuda")
+    L = launch()
+    wx.fill_synthetic(price.data_ptr(), wx.FLOAT32, n, 1, 0, 0.0, 40.0, L)
+    wx.fill_synthetic(key.data_ptr(), wx.INT32, n, 3, 1, 0, nk - 1, L)
+    table = wx.Table(n, [wx.Column("price", wx.FLOAT32, price.data_ptr()),
+                         wx.Column("quantity", wx.INT32, key.data_ptr())])
+    cap = 1 << 20
+    keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+    sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+    g = wx.group_sum(table, "price[idx]", "quantity[idx]", None, L, 0, cap, keys.data_ptr(), sums.data_ptr(),
+                     cnts.data_ptr())
+    rsum = torch.zeros(nk, dtype=torch.float64, device="cuda")
+    rcnt = torch.zeros(nk, dtype=torch.int64, device="cuda")
+    for lo in range(0, n, CHUNK):
+        kk = key[lo:lo + CHUNK].long()
+        rsum += torch.bincount(kk, weights=price[lo:lo + CHUNK].double(), minlength=nk)
+        rcnt += torch.bincount(kk, minlength=nk)
+    present = torch.nonzero(rcnt).flatten()
+    assert g == present.numel()
+    assert torch.equal(keys[:g].long(), present)
+    assert torch.equal(cnts[:g], rcnt[present])
+    assert torch.allclose(sums[:g], rsum[present], rtol=1e-12, atol=0)
+    del price, key
+    torch.cuda.empty_cache()
+
+
 def _multiset(t):
     """(sum, sum of squares) of the 32-bit patterns, as int64 (wrapping), chunk by chunk."""
     s = q = 0
