@@ -493,10 +493,13 @@ def main_ranks(args):
     def timed(step_fn, warm_s=0.0, sq_ex=None):
         """W warm-up steps (secondary lines: and at least warm_s seconds of
         them), then exactly K steps between barrier + synchronize;
-        (elapsed s, average timed-kernel ms, launches, exchange ms), max over
-        ranks.  With sq_ex (a ShardedQuery) the timed steps also record HIP
-        events around each exchange (collective + device merge): its average
-        is the fourth value (None on one rank)."""
+        (elapsed s, average timed-kernel ms, launches, exchange ms, host
+        issue ms per step), max over ranks.  With sq_ex (a ShardedQuery), up
+        to 50 more steps AFTER the timed region record events around each
+        exchange (collective + device merge): its average is the fourth value
+        (None on one rank).  Those events stay out of the timed steps: an
+        event record with the default system-scope fence costs several us
+        of stream time, ~10 % of a 1.25e8-row GROUP BY step."""
         for _ in range(args.warmup):
             step_fn()
         if warm_s > 0:
@@ -517,8 +520,6 @@ def main_ranks(args):
                 step_fn()
         wx.check(L)
         wx.timing_read()  # discard the warm-up launches
-        if sq_ex is not None:
-            sq_ex.time_exchanges(args.steps)
         mark("timed steps")
         if coll:
             dist.barrier()
@@ -526,6 +527,7 @@ def main_ranks(args):
         t0 = time.perf_counter()
         for _ in range(args.steps):
             step_fn()
+        issued = time.perf_counter() - t0  # the host's time to issue the K steps
         torch.cuda.synchronize()
         if coll:
             dist.barrier()
@@ -533,16 +535,24 @@ def main_ranks(args):
         k_ms, nl = wx.timing_read()
         wx.check(L)
         k_avg = k_ms / max(1, nl)
-        ex_ms = sq_ex.exchange_ms() if sq_ex is not None else None
+        ex_ms = None
+        if sq_ex is not None and coll:  # exchange time: more steps after the timed region (same count on every rank)
+            sq_ex.time_exchanges(min(50, args.steps))
+            for _ in range(min(50, args.steps)):
+                step_fn()
+            ex_ms = sq_ex.exchange_ms()
+            wx.timing_read()
+            wx.check(L)
         if coll:
-            t = torch.tensor([el, k_avg, -1.0 if ex_ms is None else ex_ms], dtype=torch.float64, device="cuda")
+            t = torch.tensor([el, k_avg, -1.0 if ex_ms is None else ex_ms, issued], dtype=torch.float64,
+                             device="cuda")
             wd.all_reduce_(t, op=dist.ReduceOp.MAX)
-            el, k_avg = float(t[0]), float(t[1])
+            el, k_avg, issued = float(t[0]), float(t[1]), float(t[3])
             ex_ms = None if float(t[2]) < 0 else round(float(t[2]), 4)
-        return el, k_avg, nl, ex_ms
+        return el, k_avg, nl, ex_ms, round(issued / max(1, args.steps) * 1e3, 4)
 
     mark("warm-up")
-    elapsed, kern_avg_ms, launches, ex_main = timed(step, sq_ex=sq)
+    elapsed, kern_avg_ms, launches, ex_main, issue_main = timed(step, sq_ex=sq)
 
     # algorithmic bytes per launch of the dominant kernel
     passing = int(counts.item()) if workload == "project" else None
@@ -583,6 +593,10 @@ def main_ranks(args):
                                        "topk": "all-gather 520 B per shard, wx_topk_merge",
                                        "dense": "none", "sort": "none"}[workload] if coll else "none (1 GPU)",
                           "parallelism": f"row-sharded x{world}, one process per GPU"}
+        if coll:
+            line["config"]["collectives"] = ("RCCL on the query stream (the rank's own communicator, "
+                                             "include/warpcomm.h)" if sq.stream_comm else
+                                             f"torch.distributed ({dist.get_backend()})")
         if passing is not None:
             line["config"]["passing_rows_per_gpu"] = passing
         if workload == "sort":
@@ -592,6 +606,7 @@ def main_ranks(args):
         line["check"] = check
         if ex_main is not None:
             line["exchange_ms"] = ex_main
+        line["host_issue_ms"] = issue_main
         if workload == "group":
             line["config"]["distinct_keys"] = args.keys
         line["roofline"] = roofline(bytes_per_launch, kern_avg_ms, n * rb, kname, pmc_traffic(workload, n, args.keys),
@@ -606,7 +621,7 @@ def main_ranks(args):
         self-check; `bytes_fn()` gives the dominant kernel's algorithmic
         bytes per launch on this rank (max over ranks is the kernel time)."""
         mark(f"secondary {key}")
-        el_x, k_ms_x, _, ex_x = timed(step_fn, SECONDARY_WARM_S, sq_ex=sqx)
+        el_x, k_ms_x, _, ex_x, issue_x = timed(step_fn, SECONDARY_WARM_S, sq_ex=sqx)
         chk_x = None if args.no_check else self_check(wname, sqx, cols_x, n_x, world, wd, torch)
         d = {"query": WORKLOADS[wname][0]}
         d.update(extra or {})
@@ -616,6 +631,7 @@ def main_ranks(args):
                   "frac": round(bytes_fn() / (k_ms_x * 1e-3) / 1e9 / HBM_PEAK_GBS, 4), "check": chk_x})
         if ex_x is not None:
             d["exchange_ms"] = ex_x
+        d["host_issue_ms"] = issue_x
         secondary[key] = d
 
     if workload == "project" and not args.no_secondary:
@@ -714,6 +730,8 @@ def main_ranks(args):
         line["cpu_baseline"] = cpu_leg(args, workload) if world == 1 else None
         print(json.dumps(line), flush=True)
     if coll:
+        torch.cuda.synchronize()
+        wd.release_stream_comms()
         dist.destroy_process_group()
 
 

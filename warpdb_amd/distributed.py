@@ -85,9 +85,105 @@ def _dev(group=None) -> torch.device:
     return torch.device("cuda", torch.cuda.current_device())
 
 
+# ----------------------------------------------- the exchange's own stream
+# One RCCL communicator per rank (include/warpcomm.h, libwarpdb) whose
+# collectives are enqueued on the caller's current stream -- the stream the
+# partials and merge kernels run on -- instead of torch.distributed's
+# internal one (two cross-stream event waits per exchange, ~14 us of a
+# 160-us C3-strong step, profiles/r04/c3_step_probe.txt).  Built once per
+# process group by enable_stream_comm (a collective: ShardedQuery calls it on
+# every rank); WARPDB_STREAM_COMM=0 keeps torch.distributed's collectives.
+_COMMS = {}  # process-group key -> _warpcomm.Comm, or None (torch.distributed)
+_COMM_DT = {torch.float64: 3, torch.int64: 1, torch.float32: 2, torch.int32: 0}  # wx_dtype
+
+
+def _gkey(group):
+    return "WORLD" if group is None else id(group)
+
+
+def stream_comm(group=None):
+    """This rank's own communicator for `group`, or None."""
+    return _COMMS.get(_gkey(group))
+
+
+def enable_stream_comm(group=None) -> bool:
+    """Collective over `group` (every rank calls it, once per group): build
+    this rank's RCCL communicator on the device of the current stream.  Only
+    when the exchanges would run on RCCL anyway (a device process group with
+    something to exchange).  Ranks agree before and after the build, so
+    either every rank uses its own communicator or none does (then the
+    exchanges stay on torch.distributed, with a warning)."""
+    key = _gkey(group)
+    if key in _COMMS:
+        return _COMMS[key] is not None
+    _COMMS[key] = None
+    if _single(group) or _host_staged(group) or os.environ.get("WARPDB_STREAM_COMM", "1") == "0":
+        return False
+    from . import _warpcomm as wc
+
+    def agree(ok: bool) -> bool:
+        t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        return float(t.item()) == 1.0
+
+    why = None
+    cid = bytes(wc.ID_BYTES)
+    try:
+        wc.load()
+        if dist.get_rank(group) == 0:
+            cid = wc.unique_id()
+    except Exception as e:  # noqa: BLE001 - reported below, every rank falls back together
+        why = e
+    if not agree(why is None):
+        import warnings
+
+        warnings.warn(f"own RCCL communicator unavailable ({why or 'on another rank'}): "
+                      "exchanges use torch.distributed", RuntimeWarning)
+        return False
+    idt = torch.tensor(list(cid), dtype=torch.uint8, device="cuda")
+    dist.broadcast(idt, src=0 if group is None else dist.get_global_rank(group, 0), group=group)
+    comm = None
+    try:
+        comm = wc.Comm(bytes(idt.cpu().tolist()), dist.get_world_size(group), dist.get_rank(group),
+                       torch.cuda.current_device())
+    except Exception as e:  # noqa: BLE001
+        why = e
+    if not agree(comm is not None):
+        if comm is not None:
+            comm.close()
+        import warnings
+
+        warnings.warn(f"own RCCL communicator failed ({why or 'on another rank'}): exchanges use torch.distributed",
+                      RuntimeWarning)
+        return False
+    _COMMS[key] = comm
+    return True
+
+
+def release_stream_comms() -> None:
+    """Destroy the communicators enable_stream_comm built (before
+    dist.destroy_process_group; the device work using them must be done)."""
+    for key, c in list(_COMMS.items()):
+        if c is not None:
+            c.close()
+    _COMMS.clear()
+
+
+def _comm_op(op):
+    from . import _warpcomm as wc
+
+    return {dist.ReduceOp.SUM: wc.SUM, dist.ReduceOp.MAX: wc.MAX, dist.ReduceOp.MIN: wc.MIN}.get(op)
+
+
 def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM, group=None) -> torch.Tensor:
-    """In-place all-reduce of t wherever it lives (gloo stages a device tensor on the host)."""
+    """In-place all-reduce of t wherever it lives (gloo stages a device tensor
+    on the host; with this rank's own communicator, RCCL on the current stream)."""
     if _single(group):
+        return t
+    c = stream_comm(group)
+    if c is not None and t.is_cuda and t.is_contiguous() and t.dtype in _COMM_DT and _comm_op(op) is not None:
+        c.all_reduce(t.data_ptr(), t.data_ptr(), t.numel(), _COMM_DT[t.dtype], _comm_op(op),
+                     torch.cuda.current_stream().cuda_stream)
         return t
     if _host_staged(group) and t.device.type != "cpu":
         h = t.cpu()
@@ -103,6 +199,13 @@ def all_gather(t: torch.Tensor, group=None) -> torch.Tensor:
     if _single(group):
         return t.reshape(-1)
     world = dist.get_world_size(group)
+    c = stream_comm(group)
+    if c is not None and t.is_cuda:
+        src = t.reshape(-1).contiguous()
+        out = torch.empty(world * src.numel(), dtype=src.dtype, device=src.device)
+        c.all_gather(src.data_ptr(), out.data_ptr(), src.numel() * src.element_size(),
+                     torch.cuda.current_stream().cuda_stream)
+        return out
     if _host_staged(group):
         parts = [torch.empty_like(t, device="cpu") for _ in range(world)]
         dist.all_gather(parts, t.cpu(), group=group)
@@ -254,6 +357,10 @@ class ShardedQuery:
         self._grecs = {}  # capacity -> group list record and its views
         self._ex_pool = None  # exchange timing (time_exchanges): preallocated HIP events
         self._ex_next = 0
+        # the exchanges' collectives: RCCL on this stream through the rank's
+        # own communicator (a collective call: every rank builds its
+        # ShardedQuery), else torch.distributed's
+        self.stream_comm = self.exchange and enable_stream_comm(group)
 
     # --- exchange timing (bench) -------------------------------------------
     def time_exchanges(self, steps: int) -> None:
