@@ -200,6 +200,7 @@ struct WxGroupPartArgs {
   wx_i64 capacity;
   wx_i64 *n_groups_out;
   wx_u64 *ctrs;  // [1]: error bits
+  wx_u64 *diag;  // nullable; WX_GP_DIAG builds: [blockIdx][16] tile-phase times (10 ns ticks)
 };
 
 // Top-K exchange record of one shard (wx_topk_record in warpexec.h)

@@ -1791,8 +1791,35 @@ static_assert(WX_GP_TILE <= 32768, "directory words hold 16-bit run starts and l
 // registers, no rank -- with the next tile's loads in flight a kept rank
 // spills); barrier.  LDS: the tile's staged values (f32) and bins (u16) +
 // 12 B per partition.
+#ifndef WX_GP_PLACE_BATCH
+// row quads whose cursor adds go out together in the place phase (0: one
+// add and its stores at a time).  Batches measured slower: 1 / 2 / 4 quads
+// 4.40 / 4.40 / 4.33 vs 4.24 ms per 1e9 rows x 10^6 keys
+// (profiles/r04/abl_group_wide_place_batch.txt) -- the phase is bound by
+// same-address cursor adds, not by round trips
+#define WX_GP_PLACE_BATCH 0
+#endif
+#ifndef WX_GP_DIAG
+#define WX_GP_DIAG 0  // diagnostic: per-phase times of waves 0 and 15 (s_memrealtime) into wx_a.diag
+#endif
+#if WX_GP_DIAG
+#define WX_GT_PT(slot)                                                    \
+  do {                                                                    \
+    const wx_u64 wx_now = __builtin_amdgcn_s_memrealtime();               \
+    wx_pt[slot] += wx_now - wx_pt_t;                                      \
+    wx_pt_t = wx_now;                                                     \
+  } while (0)
+#else
+#define WX_GT_PT(slot) \
+  do {                 \
+  } while (0)
+#endif
 extern "C" __global__ __launch_bounds__(WX_GP_TBLOCK) void wx_group_part_tiles(WxGroupPartArgs wx_a) {
   extern __shared__ wx_u32 wx_s_dyn[];
+#if WX_GP_DIAG
+  wx_u64 wx_pt[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  wx_u64 wx_pt_t = __builtin_amdgcn_s_memrealtime();
+#endif
   float *s_val = reinterpret_cast<float *>(wx_s_dyn);                       // [WX_GP_TILE]
   unsigned short *s_bin = reinterpret_cast<unsigned short *>(s_val + WX_GP_TILE);  // [WX_GP_TILE]
   wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_bin + WX_GP_TILE);           // [P] this tile's rows of p
@@ -1850,6 +1877,7 @@ extern "C" __global__ __launch_bounds__(WX_GP_TBLOCK) void wx_group_part_tiles(W
   wx_u32 tot_prev = 0u;
   for (wx_i64 t = t_begin; t < t_end; ++t, wx_base += WX_GP_SSPAN) {
     if (t > t_begin) WX_GS_WRITE_OUT(t - 1, tot_prev)
+    WX_GT_PT(0);
     wx_u32 wx_d[WX_GP_SUNROLL][4];  // key - key_lo, or >= P << shift: not staged (failed WHERE / outside)
     wx_u32 wx_v[WX_GP_SUNROLL][4];
 #pragma unroll
@@ -1881,17 +1909,26 @@ extern "C" __global__ __launch_bounds__(WX_GP_TBLOCK) void wx_group_part_tiles(W
     // keep the next tile's loads below this tile's evaluation (hoisted above
     // it, both register sets are live at once and the kernel spills)
     __builtin_amdgcn_sched_barrier(0);
+    WX_GT_PT(1);
     {  // the next tile's loads, in flight during this tile's LDS phases
       const wx_i64 wx_cur = wx_base;
       wx_base += WX_GP_SSPAN;
       WX_GS_LOAD_TILE()
       wx_base = wx_cur;
     }
+    WX_GT_PT(2);
     __syncthreads();  // counts complete; the previous tile's write-out has read the stage
+    WX_GT_PT(3);
     if (tid < 64) {
       // wave 0: exclusive scan of the counts (lane l: partitions [l ppl, (l + 1) ppl)),
-      // the directory words and run cursors, the totals; the counts cleared
-      const int pb = lane * ppl, pe = pb + ppl < P ? pb + ppl : P;
+      // the directory words and run cursors, the totals; the counts cleared.
+      // The lane's partition range comes from a lane id computed here
+      // (mbcnt, which the compiler rematerialises): derived from a value kept
+      // across the tile loop it was spilled, and each scratch reload waited
+      // (vmcnt) behind this wave's next-tile loads -- 1.9 us of every ~12-us
+      // tile with the other 15 waves at the barrier (WX_GP_DIAG profile)
+      const int ln = (int)__builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+      const int pb = ln * ppl, pe = pb + ppl < P ? pb + ppl : P;
       wx_u32 loc = 0u;
       for (int p = pb; p < pe; ++p) loc += s_cnt[p];
       wx_u32 incl = loc;
@@ -1911,8 +1948,36 @@ extern "C" __global__ __launch_bounds__(WX_GP_TBLOCK) void wx_group_part_tiles(W
       }
       if (lane == 63) s_tile_tot = incl;
     }
+    WX_GT_PT(4);
     __syncthreads();
+    WX_GT_PT(5);
     tot_prev = s_tile_tot;
+#if WX_GP_PLACE_BATCH
+    // WX_GP_PLACE_BATCH row quads' cursor adds go out together
+    // (unconditional: a row that is not staged adds 0 to partition 0's
+    // cursor), then their stores -- one LDS round trip per batch instead of
+    // one per row
+#pragma unroll
+    for (int wx_ub = 0; wx_ub < WX_GP_SUNROLL; wx_ub += WX_GP_PLACE_BATCH) {
+      wx_u32 j[WX_GP_PLACE_BATCH][4];
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_GP_PLACE_BATCH; ++wx_u)
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e) {
+          const wx_u32 dd = wx_d[wx_ub + wx_u][wx_e];
+          const bool st = dd < wx_span;
+          j[wx_u][wx_e] = atomicAdd(&s_cur[st ? dd >> wx_a.shift : 0u], st ? 1u : 0u);
+        }
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_GP_PLACE_BATCH; ++wx_u)
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e)
+          if (wx_d[wx_ub + wx_u][wx_e] < wx_span) {
+            s_val[j[wx_u][wx_e]] = __uint_as_float(wx_v[wx_ub + wx_u][wx_e]);
+            s_bin[j[wx_u][wx_e]] = (unsigned short)(wx_d[wx_ub + wx_u][wx_e] & wx_bmask);
+          }
+    }
+#else
 #pragma unroll
     for (int wx_u = 0; wx_u < WX_GP_SUNROLL; ++wx_u)
 #pragma unroll
@@ -1922,8 +1987,18 @@ extern "C" __global__ __launch_bounds__(WX_GP_TBLOCK) void wx_group_part_tiles(W
           s_val[j] = __uint_as_float(wx_v[wx_u][wx_e]);
           s_bin[j] = (unsigned short)(wx_d[wx_u][wx_e] & wx_bmask);
         }
+#endif
+    WX_GT_PT(6);
     __syncthreads();
+    WX_GT_PT(7);
   }
+#if WX_GP_DIAG
+  if ((threadIdx.x & 63) == 0 && (threadIdx.x == 0 || threadIdx.x == WX_GP_TBLOCK - 64) && wx_a.diag) {
+    wx_u64 *d = wx_a.diag + (wx_u64)blockIdx.x * 16 + (threadIdx.x ? 8 : 0);
+    for (int i = 0; i < 8; ++i) d[i] = wx_pt[i];
+  }
+#endif
+#undef WX_GT_PT
   if (t_end > t_begin) WX_GS_WRITE_OUT(t_end - 1, tot_prev)
 #undef WX_GS_LOAD_TILE
 #undef WX_GS_WRITE_OUT
