@@ -941,6 +941,14 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #ifndef WX_TICKET_PAIR
 #define WX_TICKET_PAIR 1
 #endif
+#ifndef WX_DEEP_OPAQUE_DT
+// 1: the store phase forms its addresses from an opaque thread index (no
+// spilled per-thread pointers, no scratch reload behind the next-tile
+// loads).  Measured slower: 2244 vs 2232 us per 1e9 rows, 234.5 vs 233.5 at
+// 1e8 (profiles/r04/abl_compact_opaque_dt.txt) -- unlike the GROUP BY tile
+// pass, where the same wait held every other wave at a barrier
+#define WX_DEEP_OPAQUE_DT 0
+#endif
 #ifndef WX_DEEP_EARLY_LAST
 // 1: a workgroup's last tile is resolved in the iteration that evaluates it
 // and written together with the tile before it (one drain iteration, not
@@ -1071,18 +1079,24 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     } else if (have2 || early_prev) {
       // write one staged tile's passing rows at its resolved offset
       auto wx_store = [&](const wx_i64 excl, const wx_u32 tot, const wx_i64 tl, const int buf) {
+      // the thread's index through an empty asm: the store addresses are
+      // formed here, not hoisted out of the tile loop as per-thread pointers
+      // (those were spilled, and their scratch reloads waited -- vmcnt is one
+      // in-order counter -- behind this iteration's next-tile loads)
+      int wx_sdt = wx_dt;
+      if (WX_DEEP_OPAQUE_DT) asm volatile("" : "+v"(wx_sdt));
       const wx_i64 prev_base = wx_a.row_base + WX_TBASE(tl);
       const float *sv = s_val[buf];
       const unsigned short *so = s_off[buf];
 #if WX_DIAG_NO_STORE  // diagnostic: timing only (results invalid), the LDS stage still read
-      if (excl == -1 && wx_a.out_val) wx_a.out_val[0] = sv[wx_dt] + (float)so[wx_dt];
+      if (excl == -1 && wx_a.out_val) wx_a.out_val[0] = sv[wx_sdt] + (float)so[wx_sdt];
 #else
       const wx_i64 end = excl + (wx_i64)tot;
       wx_i64 b0 = (excl + 31) & ~(wx_i64)31;
       if (b0 > end) b0 = end;
       const wx_i64 b1 = b0 + ((end - b0) & ~(wx_i64)3);
       const int n_head = (int)(b0 - excl), n_edge = n_head + (int)(end - b1);
-      for (int j = wx_dt; j < n_edge; j += WX_DTHREADS) {
+      for (int j = wx_sdt; j < n_edge; j += WX_DTHREADS) {
         const wx_i64 pos = j < n_head ? excl + j : b1 + (j - n_head);
         const int i = (int)(pos - excl);
         if (wx_a.out_val) wx_a.out_val[pos] = sv[i];
@@ -1092,7 +1106,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
           else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
         }
       }
-      for (wx_i64 q = b0 + 4 * (wx_i64)wx_dt; q < b1; q += 4 * (wx_i64)WX_DTHREADS) {
+      for (wx_i64 q = b0 + 4 * (wx_i64)wx_sdt; q < b1; q += 4 * (wx_i64)WX_DTHREADS) {
         const int i = (int)(q - excl);
         const float v0 = sv[i], v1 = sv[i + 1], v2 = sv[i + 2], v3 = sv[i + 3];
         const wx_u32 o0 = so[i], o1 = so[i + 1], o2 = so[i + 2], o3 = so[i + 3];
