@@ -407,12 +407,26 @@ def _bench_ranks(n, workload, extra, env_extra=None):
 ])
 def test_bench_rccl_one_rank(workload, extra):
     """The multi-rank step of bench.py on a one-rank RCCL communicator
-    (WARPDB_EXCHANGE_ONE_RANK=1, default backend): torch.distributed's
-    all_reduce / all_gather_into_tensor on RCCL with the exchange buffers the
-    8-GPU run hands over (counts, {sum, count}, window + slots, top-K
-    records), the exchange kernels behind them, every line self-checked."""
+    (WARPDB_EXCHANGE_ONE_RANK=1, default backend): the rank's own RCCL
+    communicator on the query stream (include/warpcomm.h) with the exchange
+    buffers the 8-GPU run hands over (counts, {sum, count}, window + slots,
+    top-K records), the exchange kernels behind them, every line self-checked."""
     d = _bench_ranks(1, workload, extra, {"WARPDB_EXCHANGE_ONE_RANK": "1"})
     assert d["config"]["exchange"] != "none (1 GPU)", d["config"]
+    assert "own communicator" in d["config"]["collectives"], d["config"]
+
+
+@pytest.mark.parametrize("workload,extra", [
+    ("project", ["--rows", "1e7", "--no-c4", "--c3-rows", "10000001"]),
+    ("group", ["--rows", "3e6", "--keys", "3000"]),
+    ("topk", ["--rows", "1e7"]),
+])
+def test_bench_rccl_one_rank_torch_collectives(workload, extra):
+    """The same with WARPDB_STREAM_COMM=0: torch.distributed's all_reduce /
+    all_gather_into_tensor (RCCL on the process group's stream), the path
+    every rank falls back to when a communicator of its own cannot be built."""
+    d = _bench_ranks(1, workload, extra, {"WARPDB_EXCHANGE_ONE_RANK": "1", "WARPDB_STREAM_COMM": "0"})
+    assert d["config"]["collectives"].startswith("torch.distributed"), d["config"]
 
 
 @pytest.mark.parametrize("workload", ["sum", "group", "topk"])
