@@ -98,7 +98,12 @@ _COMM_DT = {torch.float64: 3, torch.int64: 1, torch.float32: 2, torch.int32: 0} 
 
 
 def _gkey(group):
-    return "WORLD" if group is None else id(group)
+    """Registry key of a process group: its name (stable for the group's
+    lifetime, unlike id(), which a new object may reuse)."""
+    if group is None:
+        return "WORLD"
+    name = getattr(group, "group_name", None)
+    return ("name", name) if name else ("id", id(group))
 
 
 def stream_comm(group=None):
