@@ -2187,6 +2187,9 @@ extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPar
 // 1e9 rows x 10^6 keys, 4 -> 4.58, 8 -> 4.65 (profiles/r04/abl_group_wide_agg.txt)
 #define WX_GP_AGG_K 6
 #endif
+#ifndef WX_GP_AGG_DIAG_NOBIN
+#define WX_GP_AGG_DIAG_NOBIN 0  // diagnostic: values only, bins made up (results invalid)
+#endif
 #ifndef WX_GP_AGG_DIAG_NOADD
 #define WX_GP_AGG_DIAG_NOADD 0  // diagnostic: loads without the LDS adds (results invalid)
 #endif
@@ -2264,7 +2267,7 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGr
       o = ok ? o + (int)j : 0;                                                                  \
       OK |= (ok ? 1u : 0u) << k;                                                                \
       V[k] = __builtin_nontemporal_load(fv + o);                                                \
-      BN[k] = __builtin_nontemporal_load(fb + o);                                               \
+      BN[k] = WX_GP_AGG_DIAG_NOBIN ? (unsigned short)(o & 4095) : __builtin_nontemporal_load(fb + o); \
     }                                                                                           \
     if (HAS) {                                                                                  \
       sj += 64 * WX_GP_AGG_K;                                                                   \
