@@ -109,6 +109,11 @@ typedef struct wx_launch {
 #define WX_F_TIME 4u      /* record HIP events around the main kernel (wx_timing_read) */
 #define WX_F_F64_COUNTS 8u /* wx_reduce_sum: d_out's count is written as a double (exact below
                             * 2^53), so ONE all-reduce of two doubles combines shards */
+#define WX_F_ROW_ORDER 16u /* wx_group_sum / wx_group_agg: each group's sum folded in ascending row
+                            * order, one double add per row -- the reference's std::map fold
+                            * (src/warpdb.cpp:373-385) to the bit, the same on every run.
+                            * Synchronous; two ordered compactions, a stable pair sort and a
+                            * per-group fold whose time grows with the largest group's rows */
 
 /* wx_project_filter modes */
 #define WX_MODE_DENSE 0      /* out_vals[row] = expr where cond holds, other rows untouched (src/jit.cpp:55-61) */

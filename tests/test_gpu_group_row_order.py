@@ -1,0 +1,129 @@
+"""GROUP BY with WX_F_ROW_ORDER: each group's sum folded in ascending row
+order, one double add per row -- the reference's std::map fold
+(src/warpdb.cpp:373-385: `g.sum += val` over the rows in order) to the bit.
+
+The ordinary GROUP BY adds a group's values in whatever order the workgroups
+and the LDS atomics take them, so its double sums can differ from the
+reference's in the last bits when the values span many binades (its tests
+compare at 1e-12).  Here the tables are built so that order matters --
+values of 1e7, 1 and 1e-3 scales mixed within every group -- and the
+row-order sums must equal the oracle's (oracle/warpdb_oracle.c, the same
+sequential double fold) bit for bit, on every path the groups can take
+(LDS window, window + general-key hash, range-partitioned), with a WHERE,
+negative and skewed keys, MIN / MAX beside the sums, and run to run.
+"""
+from __future__ import annotations
+
+import numpy as np
+import pytest
+
+import oracle_lib as ora
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+from warpdb_amd import _warpexec as wx  # noqa: E402
+from test_gpu_parity import dev_table  # noqa: E402
+
+
+def launch(flags=wx.F_ROW_ORDER):
+    return wx.make_launch(device=0, stream=torch.cuda.current_stream().cuda_stream, flags=flags)
+
+
+def spread_values(rng, n):
+    """Values over many binades: 1e7-, 1- and 1e-3-scale rows interleaved."""
+    scale = rng.choice(np.array([1e7, 1.0, 1e-3], np.float32), n)
+    return (rng.uniform(0.0, 1.0, n).astype(np.float32) * scale).astype(np.float32)
+
+
+def run(cols, cond_c, cap, agg=False, flags=wx.F_ROW_ORDER):
+    t, _ = dev_table(cols)
+    keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+    sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+    if agg:
+        mins = torch.empty(cap, dtype=torch.float32, device="cuda")
+        maxs = torch.empty(cap, dtype=torch.float32, device="cuda")
+        g = wx.group_agg(t, "price[idx]", "quantity[idx]", cond_c, launch(flags), 0, cap, keys.data_ptr(),
+                         sums.data_ptr(), cnts.data_ptr(), mins.data_ptr(), maxs.data_ptr())
+        return (g, keys[:g].cpu().numpy(), sums[:g].cpu().numpy(), cnts[:g].cpu().numpy(),
+                mins[:g].cpu().numpy(), maxs[:g].cpu().numpy())
+    g = wx.group_sum(t, "price[idx]", "quantity[idx]", cond_c, launch(flags), 0, cap, keys.data_ptr(),
+                     sums.data_ptr(), cnts.data_ptr())
+    return g, keys[:g].cpu().numpy(), sums[:g].cpu().numpy(), cnts[:g].cpu().numpy()
+
+
+def bits(a):
+    return np.asarray(a, np.float64).view(np.uint64)
+
+
+@pytest.mark.parametrize("n,keys,cond,min_rows", [
+    (300_001, (0, 1024), None, None),                  # the LDS window
+    (300_001, (0, 100_000), None, None),               # window + general-key hash
+    (300_001, (-500, 501), "(price[idx] > 0.5f)", None),  # negative keys, a WHERE
+    ((1 << 21) + 7, (0, 100_000), None, "0"),          # range-partitioned first step
+])
+def test_row_order_sums_equal_sequential_fold(n, keys, cond, min_rows, monkeypatch):
+    if min_rows is not None:
+        monkeypatch.setenv("WARPDB_GP_MIN_ROWS", min_rows)
+    rng = np.random.default_rng(n + keys[1])
+    cols = {"price": spread_values(rng, n), "quantity": rng.integers(keys[0], keys[1], n).astype(np.int32)}
+    cap = 1 << 17
+    g, k, s, c = run(cols, cond, cap)
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity",
+                               {None: None, "(price[idx] > 0.5f)": "price > 0.5"}[cond], capacity=cap)
+    assert g == len(rk)
+    assert np.array_equal(k, rk) and np.array_equal(c, rc)
+    assert np.array_equal(bits(s), bits(rs))
+
+
+def test_row_order_skewed_and_reproducible():
+    # 90 % of the rows on one key (a long dependent chain), the rest spread
+    n = 2_000_003
+    rng = np.random.default_rng(5)
+    q = np.where(rng.random(n) < 0.9, 7, rng.integers(0, 3000, n)).astype(np.int32)
+    cols = {"price": spread_values(rng, n), "quantity": q}
+    g, k, s, c = run(cols, None, 4096)
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", capacity=4096)
+    assert g == len(rk) and np.array_equal(k, rk) and np.array_equal(c, rc)
+    assert np.array_equal(bits(s), bits(rs))
+    g2, k2, s2, c2 = run(cols, None, 4096)
+    assert g2 == g and np.array_equal(bits(s2), bits(s))
+
+
+def test_row_order_with_min_max():
+    n = 200_003
+    rng = np.random.default_rng(11)
+    cols = {"price": spread_values(rng, n), "quantity": rng.integers(0, 5000, n).astype(np.int32)}
+    g, k, s, c, mn, mx = run(cols, None, 8192, agg=True)
+    rk, rs, rc, rmn, rmx = ora.group_agg(ora.HostTable(cols), "price", "quantity", capacity=8192)
+    assert g == len(rk) and np.array_equal(k, rk) and np.array_equal(c, rc)
+    assert np.array_equal(bits(s), bits(rs))
+    assert np.array_equal(mn.view(np.uint32), rmn.view(np.uint32))
+    assert np.array_equal(mx.view(np.uint32), rmx.view(np.uint32))
+
+
+def test_row_order_edge_cases():
+    rng = np.random.default_rng(3)
+    one = {"price": np.array([2.5], np.float32), "quantity": np.array([-4], np.int32)}
+    g, k, s, c = run(one, None, 16)
+    assert g == 1 and k[0] == -4 and s[0] == 2.5 and c[0] == 1
+    n = 10_000
+    cols = {"price": spread_values(rng, n), "quantity": rng.integers(0, 10, n).astype(np.int32)}
+    g, *_ = run(cols, "(price[idx] < -1.0f)", 16)  # nothing passes
+    assert g == 0
+    with pytest.raises(wx.WarpExecError):  # more groups than capacity: the same error as without the flag
+        run(cols, None, 4)
+
+
+def test_plain_sums_order_free_within_tolerance():
+    # the ordinary path on the same data: counts exact, sums within 1e-12 of
+    # the sequential fold (they may differ in the last bits -- the reason
+    # for the flag)
+    n = 300_001
+    rng = np.random.default_rng(17)
+    cols = {"price": spread_values(rng, n), "quantity": rng.integers(0, 1024, n).astype(np.int32)}
+    g, k, s, c = run(cols, None, 4096, flags=0)
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", capacity=4096)
+    assert np.array_equal(k, rk) and np.array_equal(c, rc)
+    assert np.allclose(s, rs, rtol=1e-12, atol=0)

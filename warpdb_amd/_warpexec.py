@@ -33,6 +33,7 @@ F_SYNC = 1
 F_NO_CUSTOM = 2
 F_TIME = 4
 F_F64_COUNTS = 8  # reduce_sum: count written as a double (one f64 all-reduce combines shards)
+F_ROW_ORDER = 16  # group_sum / group_agg: sums folded in row order (bit-identical to the reference's fold)
 
 GROUP_WINDOW_BINS = 2048
 GROUP_EXCHANGE_DOUBLES = 2 * GROUP_WINDOW_BINS + 1  # [sums | counts as f64 | out-of-window groups]

@@ -338,6 +338,20 @@ struct WxHeadArgs {
   wx_i64 *count_out;
 };
 
+// Row-order GROUP BY sums (WX_F_ROW_ORDER): the passing rows' values sorted
+// stably by key (row order within a key), folded per group one double add at
+// a time.
+struct WxGroupFoldArgs {
+  const int *skeys;        // [m] sorted keys
+  const float *svals;      // [m] their values, row order within a key
+  wx_i64 m;
+  const int *gkeys;        // [n_groups] the groups, ascending
+  const wx_i64 *gcounts;   // [n_groups] their row counts
+  wx_i64 n_groups;
+  double *out_sums;        // [n_groups]
+  wx_u64 *ctrs;            // [1]: error bits (a group whose rows do not match its count)
+};
+
 struct WxSortPrepArgs {
   const void *src;
   wx_u64 *keys;

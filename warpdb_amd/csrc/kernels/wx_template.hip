@@ -3492,6 +3492,42 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
   }
 }
 
+// Row-order GROUP BY sums (WX_F_ROW_ORDER, warpexec.cpp do_group_sum_rows):
+// thread g finds its group's first row in the key-sorted array (lower
+// bound), checks that exactly its count of rows carry the key, and folds
+// their values in ascending row order, one dependent double add per row --
+// the reference's std::map fold (src/warpdb.cpp:373-385) to the bit.  The
+// loads run ahead of the adds (unrolled); the adds stay in row order.
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_fold(WxGroupFoldArgs a) {
+  for (wx_i64 g = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; g < a.n_groups; g += (wx_i64)gridDim.x * WX_BLOCK) {
+    const int key = a.gkeys[g];
+    const wx_i64 c = a.gcounts[g];
+    wx_i64 lo = 0, hi = a.m;
+    while (lo < hi) {
+      const wx_i64 mid = (lo + hi) >> 1;
+      if (a.skeys[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    if (c < 1 || lo + c > a.m || a.skeys[lo + c - 1] != key || (lo + c < a.m && a.skeys[lo + c] == key)) {
+      atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+      a.out_sums[g] = 0.0;
+      continue;
+    }
+    const float *v = a.svals + lo;
+    double s = 0.0;
+    wx_i64 i = 0;
+    for (; i + 8 <= c; i += 8) {
+      float x[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) x[j] = v[i + j];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += (double)x[j];
+    }
+    for (; i < c; ++i) s += (double)v[i];
+    a.out_sums[g] = s;
+  }
+}
+
 // ORDER BY .. LIMIT heads of any length (the k > 32 form of the top-K
 // record, wx_order_head / wx_head_merge in warpexec.cpp): positions to carry
 // through the stable key sort, then the sorted head gathered into a record;
