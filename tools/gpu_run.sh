@@ -12,6 +12,7 @@
 #   pmc:NAME[:BENCH ARGS]      FETCH_SIZE and WRITE_SIZE passes (one counter block
 #                              each) over 3 steps, summarised to NAME_pmc.json
 #   py:NAME:SCRIPT [ARGS]      python3 SCRIPT ARGS > NAME.txt
+#   pyprof:NAME:SCRIPT [ARGS]  the same under rocprofv3 --kernel-trace --stats
 set -euo pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 cd "$R"
@@ -57,6 +58,16 @@ for STEP in "$@"; do
           > "$O/pmc_$NAME/$C.log" 2>&1)
       done
       python3 tools/pmc_summary.py $(find "$O/pmc_$NAME" -name "*counter_collection.csv") > "$O/${NAME}_pmc.json" ;;
+    pyprof)
+      # the script under rocprofv3 --kernel-trace --stats (NAME_kernel_stats.csv, prof_NAME/)
+      SCRIPT=${ARGS%% *}
+      SARGS=""
+      [[ "$ARGS" == *" "* ]] && SARGS=${ARGS#* }
+      # shellcheck disable=SC2086
+      (cd /tmp && timeout -k 10 500 rocprofv3 --kernel-trace --stats -d "$O/prof_$NAME" -o run --output-format csv \
+        -- python3 "$R/$SCRIPT" $SARGS > "$O/$NAME.txt" 2>&1)
+      S=$(find "$O/prof_$NAME" -name "*kernel_stats.csv" | head -n 1 || true)
+      if [ -n "$S" ]; then cp "$S" "$O/${NAME}_kernel_stats.csv"; fi ;;
     py)
       SCRIPT=${ARGS%% *}
       SARGS=""

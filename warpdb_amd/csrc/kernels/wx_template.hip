@@ -3498,8 +3498,10 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
 // their values in ascending row order, one dependent double add per row --
 // the reference's std::map fold (src/warpdb.cpp:373-385) to the bit.  The
 // loads run ahead of the adds (unrolled); the adds stay in row order.
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_fold(WxGroupFoldArgs a) {
-  for (wx_i64 g = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; g < a.n_groups; g += (wx_i64)gridDim.x * WX_BLOCK) {
+// One wave per workgroup: a few groups' chains per CU, so the chains' loads
+// spread over as many CUs as there are waves.
+extern "C" __global__ __launch_bounds__(64) void wx_group_fold(WxGroupFoldArgs a) {
+  for (wx_i64 g = (wx_i64)blockIdx.x * 64 + threadIdx.x; g < a.n_groups; g += (wx_i64)gridDim.x * 64) {
     const int key = a.gkeys[g];
     const wx_i64 c = a.gcounts[g];
     wx_i64 lo = 0, hi = a.m;

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <cctype>
 #include <cmath>
 #include <condition_variable>
@@ -495,6 +496,10 @@ std::vector<float> WarpDB::query_sql(const std::string &sql) {
     DeviceBuffer dk(table_.device, cap * 4), ds(table_.device, cap * 8), dc(table_.device, cap * 8);
     DeviceBuffer dmn(table_.device, mm ? cap * 4 : 4), dmx(table_.device, mm ? cap * 4 : 4);
     int64_t g = 0;
+    // WARPDB_GROUP_ROW_ORDER=1: each group's sum folded in row order, the
+    // reference's own fold (src/warpdb.cpp:373-385) to the bit (WX_F_ROW_ORDER)
+    const char *ro = std::getenv("WARPDB_GROUP_ROW_ORDER");
+    if (ro && std::string(ro) == "1") L.flags |= WX_F_ROW_ORDER;
     throw_on(wx_group_agg(&v.table, agg->expr->to_cuda_expr().c_str(), key->to_cuda_expr().c_str(), cond.c_str(), &L,
                           0, cap, static_cast<int32_t *>(dk.ptr), static_cast<double *>(ds.ptr),
                           static_cast<int64_t *>(dc.ptr), mm ? static_cast<float *>(dmn.ptr) : nullptr,
