@@ -2037,6 +2037,16 @@ extern "C" __global__ __launch_bounds__(WX_GP_TBLOCK) void wx_group_part_tiles(W
 #ifndef WX_GP_AGG_ORDER
 #define WX_GP_AGG_ORDER 1  // 0: aggregation items in partition order (A/B)
 #endif
+#ifndef WX_GP_AGG_XCD
+// 1: the dispatch order is dealt to the 8 XCDs in blocks (workgroups b and
+// b + 8 share an XCD): XCD x runs the x-th eighth of the items sorted by
+// first workgroup, so the neighbouring partitions' runs of the same tiles --
+// which share their boundary lines -- are read through one L2.  Measured
+// slower: 4.38 vs 4.24-4.29 ms per 1e9 rows x 10^6 keys
+// (profiles/r04/abl_group_wide_agg_xcd.txt) -- the chip-wide sweep over one
+// tile range at a time matters more than the shared boundary lines
+#define WX_GP_AGG_XCD 0
+#endif
 extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPartArgs a) {
   __shared__ wx_u32 s_w[16];
   __shared__ wx_i64 s_r[16][4];
@@ -2159,10 +2169,16 @@ extern "C" __global__ __launch_bounds__(1024) void wx_group_part_plan(WxGroupPar
     if (tid < G) s_hist[tid] = ex2;
     __syncthreads();
     const wx_i64 ni = tot < cap ? tot : cap;
+    const wx_i64 xchunk = (ni + 7) / 8;  // WX_GP_AGG_XCD: items per XCD
+    if (WX_GP_AGG_XCD) {  // slots no item maps to (ni not a multiple of 8) stay empty
+      for (wx_i64 b = tid; b < 8 * xchunk; b += 1024) a.order[b] = 0xffffffffu;
+      __syncthreads();
+    }
     for (wx_i64 i = tid; i < ni; i += 1024) {
       const wx_u32 g = s_ig0[i];
       const wx_u32 pos = atomicAdd(&s_hist[g < (wx_u32)G ? g : G - 1], 1u);
-      a.order[WX_GP_AGG_ORDER ? pos : (wx_u32)i] = (wx_u32)i;
+      const wx_u32 slot = WX_GP_AGG_XCD ? (wx_u32)((pos % xchunk) * 8 + pos / xchunk) : pos;
+      a.order[WX_GP_AGG_ORDER ? slot : (wx_u32)i] = (wx_u32)i;
     }
   }
 }
@@ -2200,8 +2216,11 @@ extern "C" __global__ __launch_bounds__(WX_GP_BLOCK) void wx_group_part_agg(WxGr
   double *s_sum = reinterpret_cast<double *>(wx_s_dyn);  // [B]
   wx_u32 *s_cnt = reinterpret_cast<wx_u32 *>(s_sum + B);  // [B]
   wx_u32 *s_dir = s_cnt + B;                              // [WX_GP_DIRCH]
-  if ((wx_i64)blockIdx.x >= *a.n_work) return;
-  const wx_i64 w = a.order[blockIdx.x];  // items in first-workgroup order (the plan's pass 3)
+  const wx_i64 nw = *a.n_work;
+  if ((wx_i64)blockIdx.x >= (WX_GP_AGG_XCD && WX_GP_AGG_ORDER ? 8 * ((nw + 7) / 8) : nw)) return;
+  const wx_u32 wo = a.order[blockIdx.x];  // items in first-workgroup order (the plan's pass 3)
+  if (wo == 0xffffffffu) return;          // an empty XCD slot (WX_GP_AGG_XCD)
+  const wx_i64 w = wo;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const wx_i64 w0 = a.work[2 * w];
