@@ -493,3 +493,45 @@ def _warpdb_multi_against_oracle(tmp_path):
     ok3, oi3, ov3 = ora.topk(hs, "price", 340, False, cond="quantity < 60", select_expr="price * quantity")
     assert np.array_equal(rows3, oi3[40:]) and np.array_equal(bits(k3), bits(ok3[40:]))
     assert np.array_equal(bits(v3), bits(ov3[40:]))
+
+
+def test_stream_comm_fallback_is_collective(monkeypatch):
+    """A rank whose own communicator cannot be built (here: the id call
+    raises) makes every rank keep torch.distributed's collectives, with a
+    warning; the exchanges then still run and agree with the local result.
+    One-rank RCCL process group in this process (WARPDB_EXCHANGE_ONE_RANK)."""
+    import torch.distributed as dist
+
+    from warpdb_amd import _warpcomm as wc
+    from warpdb_amd import distributed as wd
+
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    for k, v in {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": "1", "RANK": "0",
+                 "WARPDB_EXCHANGE_ONE_RANK": "1"}.items():
+        monkeypatch.setenv(k, v)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    try:
+        def broken():
+            raise RuntimeError("no id for this test")
+
+        monkeypatch.setattr(wc, "unique_id", broken)
+        wd.release_stream_comms()
+        with pytest.warns(RuntimeWarning, match="exchanges use torch.distributed"):
+            assert wd.enable_stream_comm() is False
+        assert wd.stream_comm() is None
+        n = 300_001
+        cols = synth.c2_table(n)
+        price = torch.from_numpy(cols["price"]).cuda()
+        sq = wd.ShardedQuery(wd.Shard({"price": price}, 0, n))
+        assert sq.exchange and not sq.stream_comm
+        s_, c_ = sq.sum("(price[idx] * 0.9f)", "(price[idx] > 20.0f)")
+        rs, rc = ora.reduce_sum(ora.HostTable({"price": cols["price"]}), "price * 0.9", "price > 20")
+        assert c_ == rc
+        assert s_ == pytest.approx(rs, rel=1e-12)
+    finally:
+        torch.cuda.synchronize()
+        wd.release_stream_comms()
+        dist.destroy_process_group()
