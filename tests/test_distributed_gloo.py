@@ -170,6 +170,9 @@ def _worker(rank: int, world: int, port: int, n: int, errq):
         from warpdb_amd import distributed as wd
 
         dist.init_process_group("gloo", rank=rank, world_size=world)
+        # host-staged exchanges build no RCCL communicator of their own (a
+        # collective decision: every rank returns the same without a call)
+        assert wd.enable_stream_comm() is False and wd.stream_comm() is None
         b, e = wd.shard_range(n, world, rank)
         full2, full3 = synth.c2_table(n), synth.c3_table(n)
         loc2 = ora.HostTable(synth.c2_table(e - b, row_base=b))
