@@ -22,7 +22,10 @@ warpdb_amd.distributed.ShardedQuery, with the exchange each result needs
 
 Scaling: --rows R is per GPU (weak, the default: 1e9); --total-rows T splits
 T rows over the GPUs (strong; C4 is `--workload sum --total-rows 8e9`).
-With --gpus N the driver runs one process per GPU under torchrun (RCCL).
+With --gpus N the driver runs one process per GPU under torchrun (RCCL): each
+rank's exchanges run on its own RCCL communicator on the query stream
+(include/warpcomm.h; `config.collectives` names it, WARPDB_STREAM_COMM=0
+keeps torch.distributed's collectives).
 
 --api runs the single-process C++ path instead (pywarpdb.ResidentShards:
 one host thread and stream per device, ncclCommInitAll over devices
@@ -31,7 +34,9 @@ topk; its per-step time includes the collective and the host read-back.
 
 Beside the headline (`secondary`, each line timed the same way and checked
 after timing; `exchange_ms` = HIP events around the collective + device merge
-on multi-rank runs): SUM and GROUP BY on the same shards, C2 at its own 1e8
+on multi-rank runs, read from up to 50 steps after the timed ones;
+`host_issue_ms` = the host's time to issue one step): SUM and GROUP BY on the
+same shards, C2 at its own 1e8
 rows per GPU, C5 (ORDER BY price DESC LIMIT 5 + discount()), and the
 strong-scaled C3 (1e9 rows) and C4 (8e9 rows) lines over all GPUs.
 
