@@ -3518,16 +3518,22 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
 // dependent double add per row -- the reference's std::map fold
 // (src/warpdb.cpp:373-385) to the bit.  The lanes stream the group's values
 // (coalesced, WX_FOLD_U chunks of 64 in flight); the chain runs over them in
-// lane order through v_readlane, so every lane holds the same running sum.
+// lane order (LDS broadcasts, or v_readlane with WX_FOLD_LDS=0), so every
+// lane holds the same running sum.
 // A chunk past the group's end is padded with +0.0, which leaves any running
 // sum unchanged (the sum starts at +0.0, so it is never -0.0).  1e9 rows x
-// 1024 keys: 12 ms (about 12 ns per dependent add); widening every lane's
-// value first and reading doubles (two readlanes per add) took 17 ms.
+// 1024 keys: 11.4 ms through LDS broadcasts (about 11 ns per dependent
+// double add: the chain itself), 12.1 ms with v_readlane per value, 17 ms
+// with every lane widened first and two readlanes per add.
 #ifndef WX_FOLD_U
 #define WX_FOLD_U 8
 #endif
+#ifndef WX_FOLD_LDS
+#define WX_FOLD_LDS 1
+#endif
 extern "C" __global__ __launch_bounds__(64) void wx_group_fold(WxGroupFoldArgs a) {
   const int lane = threadIdx.x;
+  __shared__ double s_fold[64];
   for (wx_i64 g = blockIdx.x; g < a.n_groups; g += gridDim.x) {
     const int key = a.gkeys[g];
     const wx_i64 c = a.gcounts[g];
@@ -3556,8 +3562,24 @@ extern "C" __global__ __launch_bounds__(64) void wx_group_fold(WxGroupFoldArgs a
 #pragma unroll
       for (int u = 0; u < WX_FOLD_U; ++u) {
         if (base + u * 64 >= c) break;  // wave-uniform
+#if WX_FOLD_LDS
+        // the wave's 64 values widened into LDS, then read back by every lane
+        // (same address: a broadcast), 16 at a time, ahead of their adds --
+        // only the adds are on the chain, with no SGPR hand-off per value
+        s_fold[lane] = (double)__uint_as_float(x[u]);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): one wave, LDS in order
+#pragma unroll
+        for (int jb = 0; jb < 64; jb += 16) {
+          double d[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) d[q] = s_fold[jb + q];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) s += d[q];
+        }
+#else
 #pragma unroll
         for (int j = 0; j < 64; ++j) s += (double)__uint_as_float(__builtin_amdgcn_readlane(x[u], j));
+#endif
       }
     }
     if (lane == 0) a.out_sums[g] = s;
