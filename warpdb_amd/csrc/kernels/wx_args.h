@@ -52,6 +52,9 @@ typedef unsigned int wx_u32;
 #endif
 #define WX_RS_TILE (WX_RS_BLOCK * WX_RS_ITEMS)
 #define WX_RS_EPOCHS 63
+// three-pass radix sort (wx_radix.hip): workgroup size and keys per tile
+#define WX_RX_BLOCK_THREADS 1024
+#define WX_RX_TILE_KEYS (WX_RX_BLOCK_THREADS * 16)
 #define WX_CS_EPOCHS 63  // compaction status epochs (6 bits, 0 = never written)
 
 struct WxDenseArgs {
@@ -399,6 +402,37 @@ struct WxRadixPassArgs {
   int ascending;
   wx_u32 epoch;  // 1..WX_RS_EPOCHS
   int lead;      // 1: rank lane 0's digit group by one ballot (a skewed digit); 0: one LDS add per key
+};
+
+// Three-pass radix sort (wx_radix.hip)
+struct WxRxCountArgs {
+  const wx_u32 *src;
+  wx_i64 n;
+  wx_u32 *cnt;   // [np][ranges][2048] per-range digit counts (np = 3: wx_rx_hist_*, 1: wx_rx_count_*)
+  wx_u32 *flag;  // histogram of float keys: set to 1 when a NaN or -0.0 is seen (nullable)
+  int ranges;
+  int pass;      // wx_rx_count_*: the digit counted (0, 1, 2)
+  int aligned;   // src is 16-byte aligned
+};
+
+struct WxRxScanArgs {
+  const wx_u32 *cnt;   // [blocks][ranges][2048]
+  wx_u32 *totals;      // [blocks][2048] or null
+  const wx_u32 *base;  // [blocks][2048] digit bases (with off)
+  wx_u32 *off;         // [blocks][ranges][2048] first output slot of digit d in range r, or null
+  int ranges;
+};
+
+struct WxRxPassArgs {
+  const wx_u32 *src_k;
+  wx_u32 *dst_k;
+  const wx_u32 *src_v;  // payload (pairs) or null
+  wx_u32 *dst_v;
+  const wx_u32 *off;    // [ranges][2048]
+  wx_i64 n;
+  int ranges;
+  int shift;
+  wx_u32 mask;
 };
 
 struct WxSumFinArgs {
