@@ -327,7 +327,8 @@ wx_status wx_topk_merge(const wx_topk_record *d_records, int32_t n_records, int3
  * order of wx_sort_by_key: NaN keys last, -0.0 == +0.0, ties by ascending
  * row), with select_expr's value (null: the key) and the global row
  * (row_base + row) -- written to d_record (limit <= cap).  Synchronous (the
- * sort needs the passing count).  Scratch: 16 bytes per table row.
+ * sort needs the passing count).  Scratch: 16 bytes per table row.  A shard
+ * holds at most 2^31 - 1 rows (WX_ERR_UNSUPPORTED beyond).
  *
  * wx_head_merge: the global head of n_records shard records (record order =
  * row order): the first min(limit, total) of their candidates in the same

@@ -16,6 +16,12 @@ computed:
   workload_c3w.npz SUM(price) GROUP BY quantity with int32 keys over
                    0..74 999 (about 55 000 distinct in 100 000 rows): the
                    many-key GROUP BY, same std::map aggregation
+  workload_c3o.npz SUM(price) GROUP BY quantity where the fold order
+                   matters: int32 keys 0..199 (about 500 rows each), prices
+                   of 1e7, 1 and 1e-3 scales mixed within every key (a
+                   group's values span more than a double's 53 bits), so
+                   only the reference's own row-order std::map fold gives
+                   these bits -- the fixture of WX_F_ROW_ORDER
   workload_c5.npz  ORDER BY price DESC LIMIT 32 over 100 000 rows of
                    price rounded to 0.25 (heavy ties): rows + key bits of a
                    stable sort by the reference's eval_node value
@@ -24,7 +30,9 @@ computed:
                    and check the hash, so the fixture is tied to the data)
 
 Run in the build container:
-    ./oracle/build_ref.sh && python tests/golden/make_workload_golden.py
+    ./oracle/build_ref.sh && python tests/golden/make_workload_golden.py [case ...]
+(with case names, only those fixtures are rewritten and their entries in
+workload_golden.json replaced; the others stay byte for byte)
 """
 from __future__ import annotations
 
@@ -65,6 +73,16 @@ def c3w_table(n: int):
             "quantity": synth.uniform_int(n, synth.SEED_KEY, 0, 74_999).astype(np.int32)}
 
 
+def c3o_table(n: int):
+    """price = U[0,1) x one of {1e7, 1, 1e-3} per row, quantity int32 U{0..199}:
+    every group mixes values 2^33 apart in magnitude, so its double sum
+    depends on the order of the adds."""
+    u = synth.uniform_f32(n, synth.SEED_PRICE, 0.0, 1.0)
+    scale = np.array([1e7, 1.0, 1e-3], np.float32)[synth.uniform_int(n, 4, 0, 2)]
+    return {"price": (u * scale).astype(np.float32),
+            "quantity": synth.uniform_int(n, synth.SEED_KEY, 0, 199).astype(np.int32)}
+
+
 def c5_table(n: int):
     """price U[0,40) rounded to multiples of 0.25: ~160 distinct keys, heavy ties."""
     p = synth.uniform_f32(n, synth.SEED_PRICE, 0.0, 40.0)
@@ -79,17 +97,24 @@ def run(*args) -> str:
 def main():
     if not os.path.exists(HARNESS):
         raise SystemExit("build oracle/_ref first: ./oracle/build_ref.sh")
+    only = set(sys.argv[1:])
     meta = {"source": "oracle/_ref/ref_harness over the reference's load_csv_to_host / eval_node "
                       "(src/csv_loader.cpp:49-124, src/warpdb.cpp:109-157)", "rows": N, "cases": {}}
+    if only:
+        with open(os.path.join(HERE, "workload_golden.json")) as f:
+            meta = json.load(f)
     with tempfile.TemporaryDirectory() as tmp:
         tables = {
             "c2": (synth.c2_table(N), (), None, "price * quantity WHERE price > 15"),
             "c4": (synth.c2_table(N), (), None, "price * 0.9 WHERE price > 20"),
             "c3": (synth.c3_table(N), ("quantity",), "20", None),
             "c3w": (c3w_table(N), ("quantity",), "20", None),
+            "c3o": (c3o_table(N), ("quantity",), "20", None),
             "c5": (c5_table(N), (), None, None),
         }
         for name, (cols, ints, schema, query) in tables.items():
+            if only and name not in only:
+                continue
             text = csv_text(cols, ints)
             path = os.path.join(tmp, f"{name}.csv")
             with open(path, "w") as f:
@@ -104,14 +129,14 @@ def main():
                 np.savez_compressed(os.path.join(HERE, f"workload_{name}.npz"), mask=np.packbits(mask),
                                     bits=vals.view(np.uint32))
                 case.update(query=query, generator="synth.c2_table", passing=int(len(idx)))
-            elif name in ("c3", "c3w"):
+            elif name in ("c3", "c3w", "c3o"):
                 rows = [ln.split() for ln in run("groupsum", path, "price", "quantity", schema).splitlines()]
                 np.savez_compressed(os.path.join(HERE, f"workload_{name}.npz"),
                                     keys=np.array([int(r[0]) for r in rows], np.int32),
                                     sums=np.array([float.fromhex(r[1]) for r in rows], np.float64),
                                     counts=np.array([int(r[2]) for r in rows], np.int64))
                 case.update(query="SELECT SUM(price) FROM t GROUP BY quantity",
-                            generator="synth.c3_table" if name == "c3" else "make_workload_golden.c3w_table",
+                            generator="synth.c3_table" if name == "c3" else f"make_workload_golden.{name}_table",
                             groups=len(rows))
             else:
                 rows = [ln.split() for ln in run("topk", path, "price", "32", "1").splitlines()]

@@ -297,6 +297,52 @@ def test_two_rank_exchanges_match_oracle(n):
     assert all(p.exitcode == 0 for p in procs), "\n".join(msgs)
 
 
+def _registry_worker(port: int, errq):
+    try:
+        sys.path[:0] = [ROOT, HERE]
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch.distributed as dist
+
+        from warpdb_amd import distributed as wd
+
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        assert wd.enable_stream_comm() is False and wd.stream_comm() is None
+        first = wd._COMMS["WORLD"][0]
+        dist.destroy_process_group()
+        # a new default group: the same registry key ("WORLD"), another object
+        dist.init_process_group("gloo", rank=0, world_size=1)
+        assert wd.stream_comm() is None and "WORLD" not in wd._COMMS  # the stale entry is dropped
+        assert wd.enable_stream_comm() is False and wd._COMMS["WORLD"][0] is not first
+        # an entry left by an earlier group never hands out its communicator
+        wd._COMMS["WORLD"] = (first, 1, 0, object())
+        assert wd.stream_comm() is None
+        wd._COMMS["WORLD"] = (dist.distributed_c10d._get_default_group(), 2, 0, object())  # other size
+        assert wd.stream_comm() is None
+        wd.release_stream_comms()
+        dist.destroy_process_group()
+    except BaseException as ex:  # noqa: BLE001
+        import traceback
+
+        errq.put(f"{ex!r}\n{traceback.format_exc()}")
+        raise
+
+
+def test_stream_comm_registry_follows_the_process_group():
+    """a communicator cached for one process group is never reused
+    by a later group of the same name (torch reuses names; the default group
+    is always "WORLD") -- the entry is re-checked against the group object,
+    its size and rank on every lookup."""
+    ctx = mp.get_context("spawn")
+    errq = ctx.SimpleQueue()
+    p = ctx.Process(target=_registry_worker, args=(_free_port(), errq))
+    p.start()
+    p.join(timeout=120)
+    msgs = []
+    while not errq.empty():
+        msgs.append(errq.get())
+    assert p.exitcode == 0, "\n".join(msgs)
+
+
 def test_shard_range_matches_plan():
     from warpdb_amd import distributed as wd
     from warpdb_amd import pywarpdb as pw

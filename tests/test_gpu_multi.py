@@ -257,6 +257,11 @@ def test_warpdb_multi_gpu_group_and_shared_table():
     # beyond the 32-candidate records (the sorted heads); LIMIT past the table's rows returns every row
     k, rows, v = db.query_multi_gpu_topk("SELECT price FROM test ORDER BY price DESC LIMIT 40")
     assert v.tolist() == [30.0, 20.0, 15.25, 10.5] and rows.tolist() == [3, 1, 2, 0]
+    # LIMIT 0, OFFSET at / far beyond the rows: empty, no head gathered (no allocation error)
+    for tail in ("LIMIT 0", "LIMIT 3 OFFSET 4", "LIMIT 5 OFFSET 2000000000", "LIMIT 2000000000 OFFSET 3"):
+        k, rows, v = db.query_multi_gpu_topk("SELECT price FROM test ORDER BY price DESC " + tail)
+        want = [10.5] if tail.endswith("OFFSET 3") else []
+        assert k.tolist() == want and v.tolist() == want and rows.tolist() == ([0] if want else [])
 
 
 @pytest.mark.parametrize("rows", [3, 1000])

@@ -41,6 +41,8 @@ def table(name):
         return synth.c3_table(N), ("quantity",)
     if name == "c3w":
         return mk.c3w_table(N), ("quantity",)
+    if name == "c3o":
+        return mk.c3o_table(N), ("quantity",)
     return mk.c5_table(N), ()
 
 
@@ -54,7 +56,7 @@ def compaction_fixture(name):
     return idx, f["bits"]
 
 
-@pytest.mark.parametrize("name", ["c2", "c3", "c3w", "c4", "c5"])
+@pytest.mark.parametrize("name", ["c2", "c3", "c3w", "c3o", "c4", "c5"])
 def test_regenerated_table_is_the_reference_input(name):
     cols, ints = table(name)
     text = mk.csv_text(cols, ints)
@@ -72,14 +74,43 @@ def test_oracle_equals_reference_compaction(name):
     assert np.array_equal(vals.view(np.uint32), rbits)
 
 
-@pytest.mark.parametrize("name", ["c3", "c3w"])
+@pytest.mark.parametrize("name", ["c3", "c3w", "c3o"])
 def test_oracle_equals_reference_group_by(name):
     cols, _ = table(name)
     k, s, c = ora.group_sum(ora.HostTable(cols), "price", "quantity", sem=ora.SEM_CPU)
     f = fixture(name)
     assert len(k) == META["cases"][name]["groups"]
     assert np.array_equal(k, f["keys"]) and np.array_equal(c, f["counts"])
-    assert np.array_equal(s, f["sums"])  # double sums of float values: exact here
+    assert np.array_equal(s, f["sums"])  # c3 / c3w: exact in any order; c3o: the same row-order fold
+
+
+def _fold(vals, order):
+    s = 0.0
+    for v in vals[order]:
+        s += float(v)  # one double add per value, in the given order
+    return s
+
+
+def test_c3o_sums_depend_on_the_fold_order():
+    """workload_c3o.npz tells fold orders apart: its bits are the reference's
+    row-order std::map fold (src/warpdb.cpp:373-385), and the same values
+    added in another order -- reversed, or sorted by magnitude, as an atomic
+    path's scheduling may take them -- give other bits in most groups.  So
+    the ordinary GROUP BY (atomic adds in scheduling order) is not
+    guaranteed to equal it; WX_F_ROW_ORDER must."""
+    cols, _ = table("c3o")
+    f = fixture("c3o")
+    v = cols["price"].astype(np.float64)
+    q = cols["quantity"]
+    rev = srt = 0
+    for key, ref in zip(f["keys"], f["sums"]):
+        rows = np.nonzero(q == key)[0]
+        vals = v[rows]
+        assert _fold(vals, np.arange(len(rows))) == ref  # row order: the fixture itself
+        rev += _fold(vals, np.arange(len(rows))[::-1]) != ref
+        srt += _fold(vals, np.argsort(vals, kind="stable")) != ref
+    assert len(f["keys"]) == 200 and f["counts"].min() >= 400
+    assert rev > 50 and srt > 50, (rev, srt)
 
 
 def test_oracle_equals_reference_topk():
@@ -171,6 +202,36 @@ def test_hip_many_key_group_by_equals_reference(path, monkeypatch):
     assert g == len(f["keys"]) == 55_313
     assert np.array_equal(keys[:g].cpu().numpy(), f["keys"]) and np.array_equal(cnts[:g].cpu().numpy(), f["counts"])
     assert np.array_equal(sums[:g].cpu().numpy(), f["sums"])  # few rows per key: exact in any order
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("path", ["window", "window+hash", "hash", "partitioned"])
+def test_hip_row_order_group_by_equals_reference(path, monkeypatch):
+    """WX_F_ROW_ORDER against the reference's own row-order fold on a table
+    where the order shows in the bits (workload_c3o.npz): the LDS window
+    (key_lo 0), half the keys in the general-key hash (key_lo 100), all of
+    them there (key_lo 10^6), and the range-partitioned first step (forced
+    by the WARPDB_GP_MIN_ROWS test hook)."""
+    torch = pytest.importorskip("torch")
+    from test_gpu_parity import dev_table
+    from warpdb_amd import _warpexec as wx
+
+    key_lo = {"window": 0, "window+hash": 100, "hash": 1_000_000, "partitioned": 0}[path]
+    if path == "partitioned":
+        monkeypatch.setenv("WARPDB_GP_MIN_ROWS", "0")
+    cols, _ = table("c3o")
+    t, _ = dev_table(cols)
+    cap = 1 << 17 if path == "partitioned" else 4096
+    keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+    sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+    L = wx.make_launch(device=0, stream=torch.cuda.current_stream().cuda_stream, flags=wx.F_ROW_ORDER)
+    g = wx.group_sum(t, "price[idx]", "quantity[idx]", None, L, key_lo, cap, keys.data_ptr(), sums.data_ptr(),
+                     cnts.data_ptr())
+    f = fixture("c3o")
+    assert g == len(f["keys"]) == 200
+    assert np.array_equal(keys[:g].cpu().numpy(), f["keys"]) and np.array_equal(cnts[:g].cpu().numpy(), f["counts"])
+    assert np.array_equal(sums[:g].cpu().numpy().view(np.uint64), f["sums"].view(np.uint64))
 
 
 @pytest.mark.gpu

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Wall time of GROUP BY with and without WX_F_ROW_ORDER on bench.py's C3
 table (price f32 U[0, 40), quantity int32 U{0..keys-1}), per call, and the
-row-order sums' distance from the ordinary ones.
+row-order sums' distance from the ordinary ones.  Row order runs twice: the
+key-span path (counting scatter + fold, keys spanning <= 2048) and the
+general path (compactions + radix pair sort + fold, WARPDB_GROUP_ROWS=general);
+their sums must agree bit for bit.
 
 usage: python tools/time_group_row_order.py [rows] [keys] [reps]
 """
@@ -27,7 +30,10 @@ wx.fill_synthetic(key.data_ptr(), wx.INT32, n, 3, 1, 0, nk - 1, L0)
 table = wx.Table.from_tensors(price=price, quantity=key)
 cap = max(4096, 2 * nk)
 out = {}
-for label, flags in (("plain", wx.F_SYNC), ("row-order", wx.F_ROW_ORDER | wx.F_SYNC)):
+for label, flags in (("plain", wx.F_SYNC), ("row-order", wx.F_ROW_ORDER | wx.F_SYNC),
+                     ("row-order general", wx.F_ROW_ORDER | wx.F_SYNC)):
+    if label == "row-order general":
+        os.environ["WARPDB_GROUP_ROWS"] = "general"
     ok = torch.empty(cap, dtype=torch.int32, device="cuda")
     os_ = torch.empty(cap, dtype=torch.float64, device="cuda")
     oc = torch.empty(cap, dtype=torch.int64, device="cuda")
@@ -44,9 +50,14 @@ for label, flags in (("plain", wx.F_SYNC), ("row-order", wx.F_ROW_ORDER | wx.F_S
         ts.append(time.perf_counter() - t0)
     ts.sort()
     out[label] = (ok[:g].clone(), os_[:g].clone(), oc[:g].clone())
-    print(f"{label:10s} {n} rows x {nk} keys: median {ts[len(ts) // 2] * 1e3:.2f} ms, min {ts[0] * 1e3:.2f} ms "
+    os.environ.pop("WARPDB_GROUP_ROWS", None)
+    print(f"{label:17s} {n} rows x {nk} keys: median {ts[len(ts) // 2] * 1e3:.2f} ms, min {ts[0] * 1e3:.2f} ms "
           f"({g} groups)", flush=True)
 (k0, s0, c0), (k1, s1, c1) = out["plain"], out["row-order"]
+(k2, s2, c2) = out["row-order general"]
+assert torch.equal(k1, k2) and torch.equal(c1, c2)
+assert torch.equal(s1.view(torch.int64), s2.view(torch.int64)), "the two row-order paths differ"
+print("row-order key-span path == general path, bit for bit")
 assert torch.equal(k0, k1) and torch.equal(c0, c1)
 rel = ((s1 - s0).abs() / s1.abs().clamp_min(1e-300)).max().item()
 diff = int((s1.view(torch.int64) != s0.view(torch.int64)).sum().item())

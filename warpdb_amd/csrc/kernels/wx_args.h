@@ -52,9 +52,6 @@ typedef unsigned int wx_u32;
 #endif
 #define WX_RS_TILE (WX_RS_BLOCK * WX_RS_ITEMS)
 #define WX_RS_EPOCHS 63
-// three-pass radix sort (wx_radix.hip): workgroup size and keys per tile
-#define WX_RX_BLOCK_THREADS 1024
-#define WX_RX_TILE_KEYS (WX_RX_BLOCK_THREADS * 16)
 #define WX_CS_EPOCHS 63  // compaction status epochs (6 bits, 0 = never written)
 
 struct WxDenseArgs {
@@ -404,35 +401,44 @@ struct WxRadixPassArgs {
   int lead;      // 1: rank lane 0's digit group by one ballot (a skewed digit); 0: one LDS add per key
 };
 
-// Three-pass radix sort (wx_radix.hip)
-struct WxRxCountArgs {
-  const wx_u32 *src;
-  wx_i64 n;
-  wx_u32 *cnt;   // [np][ranges][2048] per-range digit counts (np = 3: wx_rx_hist_*, 1: wx_rx_count_*)
-  wx_u32 *flag;  // histogram of float keys: set to 1 when a NaN or -0.0 is seen (nullable)
-  int ranges;
-  int pass;      // wx_rx_count_*: the digit counted (0, 1, 2)
-  int aligned;   // src is 16-byte aligned
+// Row-order GROUP BY over a key span of at most 2048 (wx_group_rows.hip)
+#define WX_RO_TILE_ROWS 8192
+#define WX_RO_THREADS 512
+struct WxRoArgs {
+  const void *col[WX_MAX_COLS];
+  wx_i64 n_rows;
+  int key_lo;
+  int span;           // the passing rows' keys lie in [key_lo, key_lo + span), span <= 2048
+  int ranges;         // static ranges of whole tiles, one workgroup each
+  wx_u32 *cnt;        // wx_ro_count: [ranges][2048] passing rows per (range, key - key_lo)
+  const wx_u32 *off;  // wx_ro_scatter: [ranges][2048] first output slot of each bin in each range
+  float *out;         // wx_ro_scatter: the passing rows' values, key-major, row order within a key
+  wx_u64 *ctrs;       // [1]: error bits (a key outside the span)
 };
 
-struct WxRxScanArgs {
-  const wx_u32 *cnt;   // [blocks][ranges][2048]
-  wx_u32 *totals;      // [blocks][2048] or null
-  const wx_u32 *base;  // [blocks][2048] digit bases (with off)
-  wx_u32 *off;         // [blocks][ranges][2048] first output slot of digit d in range r, or null
+struct WxRoScanArgs {
+  const wx_u32 *cnt;   // [ranges][2048]
+  wx_u32 *totals;      // [2048] or null
+  const wx_u32 *base;  // [2048] (with off)
+  wx_u32 *off;         // [ranges][2048] or null
   int ranges;
 };
 
-struct WxRxPassArgs {
-  const wx_u32 *src_k;
-  wx_u32 *dst_k;
-  const wx_u32 *src_v;  // payload (pairs) or null
-  wx_u32 *dst_v;
-  const wx_u32 *off;    // [ranges][2048]
-  wx_i64 n;
-  int ranges;
-  int shift;
-  wx_u32 mask;
+struct WxRoBaseArgs {
+  const wx_u32 *totals;    // [2048]
+  wx_u32 *base;            // [2048] exclusive prefix of the totals
+  const int *gkeys;        // [n_groups] the ordinary call's groups
+  const wx_i64 *gcounts;   // [n_groups]
+  wx_i64 n_groups;
+  int key_lo;
+  wx_u64 *ctrs;            // [1]: error bits (counts that do not match)
+};
+
+struct WxRoFoldArgs {
+  const float *svals;      // the key-major values (group g's rows after the groups before it)
+  const wx_i64 *gcounts;   // [n_groups]
+  wx_i64 n_groups;
+  double *out_sums;        // [n_groups]
 };
 
 struct WxSumFinArgs {

@@ -298,7 +298,10 @@ warpdb::TopkResult WarpDB::query_multi_gpu_topk(const std::string &sql) {
   int64_t lim = ast.limit->count;
   if (off < 0 || lim < 0) throw std::runtime_error("query_multi_gpu_topk needs OFFSET, LIMIT >= 0");
   const int64_t n_rows = static_cast<int64_t>(host_table_.num_rows());
-  if (off + lim > n_rows) lim = std::max<int64_t>(0, n_rows - off);  // nothing beyond the table
+  // nothing beyond the table: LIMIT 0 or OFFSET >= rows is an empty result
+  // (no head is gathered); otherwise off + lim <= rows, computed without
+  // overflow, so each shard's head record holds at most the table's rows
+  lim = off >= n_rows ? 0 : std::min(lim, n_rows - off);
   const auto cols = names_of(host_table_);
   validate_ast(ast.select_list[0].get(), cols);
   validate_ast(ast.order_by->expr.get(), cols);
@@ -308,7 +311,7 @@ warpdb::TopkResult WarpDB::query_multi_gpu_topk(const std::string &sql) {
     cond = (*ast.where)->to_cuda_expr();
   }
   warpdb::TopkResult r;
-  if (off + lim == 0) return r;
+  if (lim == 0) return r;
   r = shards().topk(ast.order_by->expr->to_cuda_expr(), cond, ast.select_list[0]->to_cuda_expr(), off + lim,
                     !ast.order_by->ascending);
   const size_t drop = std::min(r.keys.size(), static_cast<size_t>(off));  // OFFSET

@@ -93,7 +93,12 @@ def _dev(group=None) -> torch.device:
 # 160-us C3-strong step, profiles/r04/c3_step_probe.txt).  Built once per
 # process group by enable_stream_comm (a collective: ShardedQuery calls it on
 # every rank); WARPDB_STREAM_COMM=0 keeps torch.distributed's collectives.
-_COMMS = {}  # process-group key -> _warpcomm.Comm, or None (torch.distributed)
+# process-group key -> (the group object, world size, rank, _warpcomm.Comm or
+# None = torch.distributed's collectives).  The group object is held, so a
+# later process group of the same name (torch reuses names, and the default
+# group is always "WORLD") is a different object: the entry is then stale and
+# dropped on lookup instead of handing out a communicator with other peers.
+_COMMS = {}
 _COMM_DT = {torch.float64: 3, torch.int64: 1, torch.float32: 2, torch.int32: 0}  # wx_dtype
 
 
@@ -106,9 +111,31 @@ def _gkey(group):
     return ("name", name) if name else ("id", id(group))
 
 
+def _gobj(group):
+    return dist.distributed_c10d._get_default_group() if group is None else group
+
+
+def _entry(group):
+    """The registry entry of `group` if it was built for this very process
+    group (same object, size and rank); a stale entry is dropped.  Its
+    communicator is not destroyed here: its peers may be gone, and a
+    destroy could wait on them (release_stream_comms before
+    dist.destroy_process_group is the clean path)."""
+    key = _gkey(group)
+    e = _COMMS.get(key)
+    if e is None:
+        return None
+    g, n, r, _ = e
+    if g is not _gobj(group) or n != dist.get_world_size(group) or r != dist.get_rank(group):
+        del _COMMS[key]
+        return None
+    return e
+
+
 def stream_comm(group=None):
     """This rank's own communicator for `group`, or None."""
-    return _COMMS.get(_gkey(group))
+    e = _entry(group)
+    return e[3] if e else None
 
 
 def enable_stream_comm(group=None) -> bool:
@@ -119,9 +146,10 @@ def enable_stream_comm(group=None) -> bool:
     either every rank uses its own communicator or none does (then the
     exchanges stay on torch.distributed, with a warning)."""
     key = _gkey(group)
-    if key in _COMMS:
-        return _COMMS[key] is not None
-    _COMMS[key] = None
+    e = _entry(group)
+    if e is not None:
+        return e[3] is not None
+    _COMMS[key] = (_gobj(group), dist.get_world_size(group), dist.get_rank(group), None)
     if _single(group) or _host_staged(group) or os.environ.get("WARPDB_STREAM_COMM", "1") == "0":
         return False
     from . import _warpcomm as wc
@@ -161,16 +189,17 @@ def enable_stream_comm(group=None) -> bool:
         warnings.warn(f"own RCCL communicator failed ({why or 'on another rank'}): exchanges use torch.distributed",
                       RuntimeWarning)
         return False
-    _COMMS[key] = comm
+    _COMMS[key] = (_gobj(group), dist.get_world_size(group), dist.get_rank(group), comm)
     return True
 
 
 def release_stream_comms() -> None:
-    """Destroy the communicators enable_stream_comm built (before
-    dist.destroy_process_group; the device work using them must be done)."""
-    for key, c in list(_COMMS.items()):
-        if c is not None:
-            c.close()
+    """Destroy the communicators enable_stream_comm built.  Call it before
+    dist.destroy_process_group (the device work using them must be done); an
+    entry left behind is never reused by a later process group (see _entry)."""
+    for key, e in list(_COMMS.items()):
+        if e[3] is not None:
+            e[3].close()
     _COMMS.clear()
 
 
