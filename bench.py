@@ -97,7 +97,8 @@ def parse():
     p.add_argument("--total-rows", type=float, default=None, help="rows over all GPUs (strong scaling)")
     p.add_argument("--workload", choices=sorted(WORKLOADS), default="project")
     p.add_argument("--api", action="store_true", help="single-process C++ multi-GPU path (sum, group)")
-    p.add_argument("--cpu-sample", type=float, default=5e7, help="rows for the CPU baseline sample")
+    p.add_argument("--cpu-sample", type=float, default=1e8,
+                   help="rows for the CPU baseline sample (BASELINE.md's plan: 1e8)")
     p.add_argument("--cpu-threads", type=int, default=0, help="threads of the all-cores CPU run (0: all)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-check", action="store_true", help="skip the post-timing result check")
@@ -146,6 +147,16 @@ def cpu_threads_default() -> int:
     return host_info()["usable_cpus"] or 1
 
 
+def cores_reason(threads: int, info: dict) -> str:
+    """Why the all-cores leg ran on `threads` threads."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) == threads and info.get("usable_cpus", 0) > threads:
+        return (f"this one-GPU job's CPU share: the pool sets OMP_NUM_THREADS={env} per GPU; the host's "
+                f"{info.get('usable_cpus')} logical CPUs are shared with the other GPUs' jobs, so more threads "
+                f"would time other tenants' work, not the reference's")
+    return f"every usable CPU of the host ({info.get('usable_cpus')})"
+
+
 def cpu_sort_baseline(sample: int):
     """ORDER BY on the host: the sample's values stable-sorted by numpy on one
     core (the reference's own sort is a one-thread GPU bubble sort,
@@ -185,8 +196,10 @@ def cpu_baseline(query: str, sample: int, threads: int):
             if threads > 1:
                 mt = run(threads)
                 if mt:
+                    info = host_info()
                     out["all_cores"] = {"value": round(mt["rows_per_s"], 1), "unit": "rows/s", "cores": threads,
-                                        "seconds": round(mt["seconds"], 3)}
+                                        "seconds": round(mt["seconds"], 3),
+                                        "why_cores": cores_reason(threads, info)}
             return out
     import numpy as np
 
@@ -775,10 +788,21 @@ def main_api(args):
 
     for _ in range(args.warmup):
         step()
+    shards.take_timing()  # discard the warm-up's (nothing is timed yet)
+    shards.set_timing(True, False)  # HIP events around each shard's main kernel (no system fence)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     elapsed = time.perf_counter() - t0
+    shards.set_timing(False, False)
+    kt = shards.take_timing()
+    # the exchange (collective + merge, an event pair per device) from more
+    # steps after the timed region, as the torchrun line reads exchange_ms
+    shards.set_timing(False, True)
+    for _ in range(min(50, args.steps)):
+        step()
+    shards.set_timing(False, False)
+    ex_ms = shards.take_timing()["exchange_ms"]
     n_max = max(e - b for _, b, e in shards.ranges())
     line = line_common(args, shards.num_shards, n_total, elapsed, workload)
     line["config"] = {"workload": f"{query} ({workload})", "rows_per_gpu": n_max, "total_rows": n_total,
@@ -791,12 +815,15 @@ def main_api(args):
                                   if shards.num_shards > 1 or os.environ.get("WARPDB_EXCHANGE_ONE_RANK") == "1"
                                   else "none (1 GPU)",
                       "parallelism": f"row-sharded x{shards.num_shards}, one process, one thread + stream per GPU"}
-    # the C++ path has no per-kernel events: the whole step bounds the kernel
-    ms = elapsed / args.steps * 1e3
     rb = READ_BYTES[workload]
-    line["roofline"] = roofline(n_max * rb, ms, n_max * rb, kname, pmc_traffic(workload, n_max),
-                                "whole step (kernel + all-reduce + host read-back): a lower bound on the kernel")
-    line["check"] = api_check(workload, step(), n_total)
+    kern_ms = kt["kernel_ms"] if kt["launches"] else elapsed / args.steps * 1e3
+    line["roofline"] = roofline(n_max * rb, kern_ms, n_max * rb, kname, pmc_traffic(workload, n_max),
+                                "HIP events around each shard's main kernel on its device's stream "
+                                "(ResidentShards.set_timing, WX_F_TIME), average over the timed steps, slowest device"
+                                if kt["launches"] else "whole step (no kernel events were read)")
+    line["kernel_launches"] = kt["launches"]
+    line["exchange_ms"] = None if ex_ms is None else round(ex_ms, 4)
+    line["check"] = api_check(workload, step(), n_total, shards)
     line["cpu_baseline"] = cpu_leg(args, workload) if shards.num_shards == 1 else None
     print(json.dumps(line), flush=True)
 
@@ -809,26 +836,73 @@ def api_group_doubles(shards):
     return wx.group_slots_doubles(shards, max(1, min(64, 4096 // shards)))
 
 
-def api_check(workload, res, n_total):
-    """Size-independent properties of the C++ path's result (its data lives
-    inside ResidentShards): the tests pin the values themselves."""
+def api_check(workload, res, n_total, shards):
+    """The C++ path's result against torch on the same rows, regenerated on
+    the first GPU chunk by chunk (the shards' synthetic columns come from the
+    same counter-based generator, wx_fill_synthetic, at their global row
+    numbers): the torchrun line's checks -- counts exact, sums within 1e-12
+    relative, top-5 keys the order statistics and discount() values
+    bit-equal."""
     import numpy as np
+    import torch
+
+    from warpdb_amd import _warpexec as wx
+
+    L = wx.make_launch(stream=torch.cuda.current_stream().cuda_stream)
+    spec = {c[0]: c for c in columns_for(workload)}
+
+    def chunks():
+        for c0 in range(0, n_total, CHECK_CHUNK):
+            c1 = min(n_total, c0 + CHECK_CHUNK)
+            out = {}
+            for nm, (_, dt, seed, kind, lo, hi) in spec.items():
+                t = torch.empty(c1 - c0, dtype=torch.float32 if dt == wx.FLOAT32 else torch.int32, device="cuda")
+                wx.fill_synthetic(t.data_ptr(), dt, c1 - c0, seed, kind, lo, hi, L, row_base=c0)
+                out[nm] = t
+            yield c0, c1, out
 
     if workload == "sum":
-        s, c = res
-        if not (0 < c <= n_total and s > 0):
-            raise SystemExit(f"check failed: SUM {s} / {c}")
-        return f"ok: count {c} of {n_total} rows, sum {s:.6e}"
+        got_s, got_c = res
+        acc = [0.0, 0]
+        for _, _, c in chunks():
+            p_ = c["price"]
+            m = p_ > 20.0
+            acc[0] += torch.where(m, p_ * 0.9, torch.zeros_like(p_)).double().sum().item()
+            acc[1] += int(m.sum().item())
+        if got_c != acc[1] or abs(got_s - acc[0]) > 1e-12 * abs(acc[0]):
+            raise SystemExit(f"check failed: SUM {got_s} / {got_c} vs {acc[0]} / {acc[1]}")
+        return f"ok: count {got_c} exact, sum {got_s:.6e} within 1e-12 of torch"
     if workload == "group":
-        k, s, c = res
-        if int(np.asarray(c).sum()) != n_total or not bool(np.all(np.diff(np.asarray(k)) > 0)):
-            raise SystemExit("check failed: GROUP BY counts do not add up to the rows, or keys not ascending")
-        return f"ok: {len(k)} groups, counts add up to {n_total}, keys ascending"
-    k, rows, v = (np.asarray(x) for x in res)
-    want = (k.astype(np.float32) * np.float32(0.9)).astype(np.float32)
-    if len(k) != 5 or not bool(np.all(np.diff(k) <= 0)) or not np.array_equal(v.view(np.uint32), want.view(np.uint32)):
-        raise SystemExit("check failed: top-K keys not descending or discount() values differ")
-    return "ok: 5 keys descending, discount() values bit-equal"
+        gk, gs, gc = (np.asarray(x) for x in res)
+        keys = int(spec["quantity"][5]) + 1
+        ws = torch.zeros(keys, dtype=torch.float64, device="cuda")
+        wc = torch.zeros(keys, dtype=torch.float64, device="cuda")
+        for _, _, c in chunks():
+            kk = c["quantity"].long()
+            ws += torch.bincount(kk, weights=c["price"].double(), minlength=keys)[:keys]
+            wc += torch.bincount(kk, minlength=keys)[:keys].double()
+        ws, wc = ws.cpu().numpy(), wc.cpu().numpy()
+        present = np.nonzero(wc > 0)[0]
+        if not np.array_equal(gk.astype(np.int64), present) or not np.array_equal(gc.astype(np.float64), wc[present]):
+            raise SystemExit("check failed: GROUP BY keys / counts differ from torch")
+        rel = np.abs(gs - ws[present]) / np.maximum(np.abs(ws[present]), 1e-300)
+        if len(rel) and float(rel.max()) > 1e-12:
+            raise SystemExit("check failed: GROUP BY sums differ from torch beyond 1e-12")
+        return f"ok: {len(gk)} groups, keys and counts exact, sums within 1e-12 of torch"
+    tk, rows, tv = (np.asarray(x) for x in res)
+    above = [0] * len(tk)
+    at = [0] * len(tk)
+    for _, _, c in chunks():
+        p_ = c["price"]
+        for i, t in enumerate(tk.tolist()):
+            above[i] += int((p_ > float(t)).sum())
+            at[i] += int((p_ >= float(t)).sum())
+    if len(tk) != 5 or any(above[i] > i or at[i] < i + 1 for i in range(5)):
+        raise SystemExit(f"check failed: top-5 keys {tk.tolist()}")
+    want = (tk.astype(np.float32) * np.float32(0.9)).astype(np.float32)
+    if not np.array_equal(tv.view(np.uint32), want.view(np.uint32)):
+        raise SystemExit("check failed: discount(price, 0.9) values differ")
+    return "ok: top-5 keys are the order statistics, discount() values bit-equal"
 
 
 def main():

@@ -45,6 +45,16 @@ struct TopkResult {
   std::vector<float> values;
 };
 
+// Timing of the resident-shard queries (bench.py --api): the main kernel of
+// each shard (HIP events around it, WX_F_TIME) and the exchange (events on
+// each shard's stream around the collective and the merge after it).
+struct ApiTiming {
+  double kernel_ms = 0;     // average main-kernel time per launch, the slowest device's
+  int64_t launches = 0;     // main-kernel launches of that device since the last read
+  double exchange_ms = -1;  // average collective + merge time per query, the slowest device's (-1: none ran)
+  int64_t exchanges = 0;
+};
+
 // One synthetic column (wx_fill_synthetic's counter-based generator, so each
 // device generates its own rows at their global row numbers).
 struct SyntheticColumn {
@@ -89,6 +99,12 @@ class ResidentShards {
   // the records and the merge on the first shard's device
   TopkResult topk(const std::string &order_cuda, const std::string &cond_cuda, const std::string &select_cuda,
                   int64_t k, bool descending) const;
+  // time the next queries' main kernels (WX_F_TIME) and / or their
+  // exchanges (an event pair per device and query; only where a collective
+  // runs: more than one shard, or the one-rank hook)
+  void set_timing(bool kernels, bool exchange);
+  // what was timed since the last read; the recorded events are released
+  ApiTiming take_timing();
 
  private:
   ResidentShards();

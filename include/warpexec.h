@@ -393,8 +393,11 @@ wx_status wx_prepare(const wx_table *table, int32_t op, const char *expr, const 
 wx_status wx_check(const wx_launch *launch, char *err, size_t errlen);
 
 /* Sum of the HIP-event durations of the main kernels launched with WX_F_TIME
- * on this thread since the last read (synchronises on the recorded events). */
+ * (by any thread of the process) since the last read, and their number
+ * (synchronises on the recorded events).  _device: only those launched on
+ * `device`; the others stay for a later read. */
 wx_status wx_timing_read(double *total_ms, int64_t *launches, char *err, size_t errlen);
+wx_status wx_timing_read_device(int32_t device, double *total_ms, int64_t *launches, char *err, size_t errlen);
 
 /* Kernel-cache statistics: compiled modules and hits since load. */
 void wx_cache_stats(int64_t *compiles, int64_t *hits);

@@ -180,14 +180,10 @@ def test_compact_c2_shape_vs_oracle(n, sched, monkeypatch):
     assert np.array_equal(bits(vals), bits(rv))
 
 
-@pytest.mark.parametrize("half_tail", ["0", "1", "2", "5"])
-@pytest.mark.parametrize("n", [3_158_017, 4_000_003, 7_777_777, 12_582_912])
-def test_compact_half_height_tail_vs_oracle(n, half_tail, monkeypatch):
-    # the deep kernel's last tiles are half height (about WARPDB_COMPACT_HALF_TAIL
-    # per workgroup; on 256 CUs 2 x 256 x 6144 rows + one tile is the smallest
-    # table with a tail): row ranges of mixed tiles, a ragged last half tile,
-    # and the stores' row base of a half tile
-    monkeypatch.setenv("WARPDB_COMPACT_HALF_TAIL", half_tail)
+@pytest.mark.parametrize("n", [3_158_017, 12_582_912])
+def test_compact_many_tiles_row_base_vs_oracle(n):
+    # more tiles than workgroups (several pipeline iterations each), a ragged
+    # or whole last tile, and a row base in the stored indices
     cols = synth.c2_table(n, row_base=77)
     table, _ = dev_table(cols)
     vals, idx = gpu_compact(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", row_base=77)

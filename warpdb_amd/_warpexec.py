@@ -90,6 +90,7 @@ EXPORTED_SYMBOLS = (
     "wx_prepare",
     "wx_check",
     "wx_timing_read",
+    "wx_timing_read_device",
     "wx_cache_stats",
     "wx_shutdown",
     "wx_abi_version",
@@ -171,6 +172,7 @@ def load() -> ctypes.CDLL:
         "wx_prepare": [T, I32, E, E, E, I32, L, E, S, E, S],
         "wx_check": [L, E, S],
         "wx_timing_read": [pD, pI64, E, S],
+        "wx_timing_read_device": [I32, pD, pI64, E, S],
     }
     for name, argtypes in sig.items():
         fn = getattr(lib, name)
@@ -514,11 +516,16 @@ def check(launch: WxLaunch) -> None:
     _check(lib.wx_check(ctypes.byref(launch), err, len(err)), err)
 
 
-def timing_read():
+def timing_read(device: Optional[int] = None):
+    """(total ms, launches) of the unread WX_F_TIME launches of the process
+    (of `device` only, when given)."""
     lib = load()
     err = _err()
     ms, n = ctypes.c_double(0), ctypes.c_int64(0)
-    _check(lib.wx_timing_read(ctypes.byref(ms), ctypes.byref(n), err, len(err)), err)
+    if device is None:
+        _check(lib.wx_timing_read(ctypes.byref(ms), ctypes.byref(n), err, len(err)), err)
+    else:
+        _check(lib.wx_timing_read_device(device, ctypes.byref(ms), ctypes.byref(n), err, len(err)), err)
     return ms.value, n.value
 
 

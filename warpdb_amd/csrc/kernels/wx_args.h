@@ -70,7 +70,6 @@ struct WxCompactArgs {
   wx_i64 *count_out;  // nullable
   wx_i64 n_rows;
   wx_i64 n_tiles;
-  wx_i64 n_full;  // deep kernel: tiles [0, n_full) hold WX_TILE rows, later ones WX_TILE / 2 (the tail)
   wx_i64 row_base;
   int idx64;
   wx_u32 epoch;  // 1..WX_CS_EPOCHS: tags this launch's status words

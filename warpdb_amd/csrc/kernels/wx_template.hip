@@ -554,10 +554,6 @@ __device__ __forceinline__ wx_u64 wx_cflag(wx_u64 w, wx_u64 E) {
 #define WX_LOAD_TILE_FULL(name, T, slot) \
   ::wx::load4_full<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4, wx_in##slot[wx_g]);
 #define WX_BIND_TILE_IN(name, T, slot) const ::wx::reg<T> name{wx_in##slot[wx_g][wx_e]};
-// the same loads bounded by the tile's own end (wx_lim: a half-height tail tile
-// loads its first WX_GROUPS / 2 groups only)
-#define WX_LOAD_TILE_LIM(name, T, slot) \
-  ::wx::load4<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4, wx_lim, wx_in##slot[wx_g]);
 
 // Exclusive prefix of `tile` from its predecessors' status words; one wave.
 // Load j of lane l reads tile look - 64*j - l: every load instruction covers
@@ -941,29 +937,13 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #ifndef WX_TICKET_PAIR
 #define WX_TICKET_PAIR 1
 #endif
-#ifndef WX_DEEP_OPAQUE_DT
-// 1: the store phase forms its addresses from an opaque thread index (no
-// spilled per-thread pointers, no scratch reload behind the next-tile
-// loads).  Measured slower: 2244 vs 2232 us per 1e9 rows, 234.5 vs 233.5 at
-// 1e8 (profiles/r04/abl_compact_opaque_dt.txt) -- unlike the GROUP BY tile
-// pass, where the same wait held every other wave at a barrier
-#define WX_DEEP_OPAQUE_DT 0
-#endif
-#ifndef WX_DEEP_EARLY_LAST
-// 1: a workgroup's last tile is resolved in the iteration that evaluates it
-// and written together with the tile before it (one drain iteration, not
-// two).  Measured slower (1e8 rows 234.9 vs 233.9 us, 1e9 2255 vs 2250 us,
-// profiles/r04/abl_compact_early_last.txt): the extra look-back holds that
-// iteration's barrier while the neighbouring tiles are still unpublished.
-#define WX_DEEP_EARLY_LAST 0
-#endif
 #if defined(WX_COMPACT_STATIC) && WX_COMPACT_STATIC == 3
-// Tile t's first row and row count: the last tiles of a launch (t >= n_full,
-// chosen by the host, WARPDB_COMPACT_HALF_TAIL per workgroup; none by
-// default) are half height.  Meant to shorten each workgroup's final
-// iterations and the spread of their ends; measured slower (warpexec.cpp).
-#define WX_TBASE(t) ((t) < wx_a.n_full ? (t) * (wx_i64)WX_TILE : wx_a.n_full * (wx_i64)WX_TILE + ((t) - wx_a.n_full) * (wx_i64)(WX_TILE / 2))
-#define WX_TROWS(t) ((t) < wx_a.n_full ? (wx_i64)WX_TILE : (wx_i64)(WX_TILE / 2))
+// (Measured and dropped, round 4, profiles/r04/: half-height tiles for each
+// workgroup's last iterations, +2 us per extra tile at 1e8 rows,
+// abl_compact_half_tail.txt; resolving a workgroup's last tile in the
+// iteration that evaluates it, 234.9 vs 233.9 us at 1e8 and 2255 vs 2250 us
+// at 1e9, abl_compact_early_last.txt; store addresses from an opaque thread
+// index, 2244 vs 2232 us at 1e9, abl_compact_opaque_dt.txt.)
 #ifndef WX_DIAG_TIMELINE
 #define WX_DIAG_TIMELINE 0  // diagnostic: per-workgroup entry / first-tile / loop-end times (diag[b * 16 ..])
 #endif
@@ -978,11 +958,9 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
   __shared__ float s_val[2][WX_TILE];
   __shared__ unsigned short s_off[2][WX_TILE];
   __shared__ wx_i64 s_excl[2];
-  __shared__ wx_i64 s_excl_last;  // the last tile's offset (WX_DEEP_EARLY_LAST)
   __shared__ wx_i64 s_tiles[4];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool control = wave == WX_DWAVES;
-  bool early_prev = false;  // the previous iteration evaluated the last tile and resolved it
   const int wx_dt = tid;
   if (tid == 0) {
     if (WX_TICKET_PAIR) {  // one dequeue for both first tiles (the counter word serialises every dequeue)
@@ -1003,10 +981,9 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
   wx_u32 tot1 = 0, tot2 = 0;       // their passing counts
   WX_COLS(WX_DECL_TILE_IN)
   if (!control && tile < wx_a.n_tiles) {
-    const wx_i64 wx_tb = WX_TBASE(tile);
-    const wx_i64 wx_lim = wx_tb + WX_TROWS(tile) < wx_a.n_rows ? wx_tb + WX_TROWS(tile) : wx_a.n_rows;
+    const wx_i64 wx_tb = tile * WX_TILE;
 #pragma unroll
-    for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_LIM) }
+    for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
   }
   for (int k = 0;; ++k) {
     const bool have = tile < wx_a.n_tiles;
@@ -1014,17 +991,14 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     const bool have2 = k >= 2 && tile2 < wx_a.n_tiles;
     if (!have && !have1 && !have2) break;
     const wx_i64 next_tile = s_tiles[(k + 1) & 3];
-    // t_k is this workgroup's last tile (the ticket of iteration k + 1 came back empty)
-    const bool last_eval = WX_DEEP_EARLY_LAST && have && next_tile >= wx_a.n_tiles;
-    const wx_i64 tile_base = WX_TBASE(tile);
+    const wx_i64 tile_base = tile * WX_TILE;
     const int cur = k & 1;  // t_k is staged in buffer cur, t_{k-2} is read from it first
     wx_u32 wx_kb = 0;
     float wx_val[WX_GROUPS][4];
     wx_u32 lane_pre[WX_GROUPS];
     // phase 1 (data): evaluate t_k, issue t_{k+1}'s loads, rank t_k
     if (!control && have) {
-      const wx_u32 wx_rows = (wx_u32)(wx_a.n_rows - tile_base < WX_TROWS(tile) ? wx_a.n_rows - tile_base
-                                                                                  : WX_TROWS(tile));
+      const wx_u32 wx_rows = (wx_u32)(wx_a.n_rows - tile_base < WX_TILE ? wx_a.n_rows - tile_base : WX_TILE);
 #pragma unroll
       for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
 #pragma unroll
@@ -1044,10 +1018,9 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
       ++wx_ntiles;
 #endif
       if (next_tile < wx_a.n_tiles) {
-        const wx_i64 wx_tb = WX_TBASE(next_tile);
-        const wx_i64 wx_lim = wx_tb + WX_TROWS(next_tile) < wx_a.n_rows ? wx_tb + WX_TROWS(next_tile) : wx_a.n_rows;
+        const wx_i64 wx_tb = next_tile * WX_TILE;
 #pragma unroll
-        for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_LIM) }
+        for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
       }
 #pragma unroll
       for (int g = 0; g < WX_GROUPS; ++g) {
@@ -1076,16 +1049,11 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
                                                                     __HIP_MEMORY_SCOPE_AGENT)
                                    : wx_a.n_tiles;
       }
-    } else if (have2 || early_prev) {
+    } else if (have2) {
       // write one staged tile's passing rows at its resolved offset
       auto wx_store = [&](const wx_i64 excl, const wx_u32 tot, const wx_i64 tl, const int buf) {
-      // the thread's index through an empty asm: the store addresses are
-      // formed here, not hoisted out of the tile loop as per-thread pointers
-      // (those were spilled, and their scratch reloads waited -- vmcnt is one
-      // in-order counter -- behind this iteration's next-tile loads)
-      int wx_sdt = wx_dt;
-      if (WX_DEEP_OPAQUE_DT) asm volatile("" : "+v"(wx_sdt));
-      const wx_i64 prev_base = wx_a.row_base + WX_TBASE(tl);
+      const int wx_sdt = wx_dt;
+      const wx_i64 prev_base = wx_a.row_base + tl * WX_TILE;
       const float *sv = s_val[buf];
       const unsigned short *so = s_off[buf];
 #if WX_DIAG_NO_STORE  // diagnostic: timing only (results invalid), the LDS stage still read
@@ -1133,14 +1101,13 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
       }
 #endif
       };
-      if (have2) wx_store(s_excl[cur], tot2, tile2, cur);  // t_{k-2} (its offset resolved in iteration k - 1)
-      if (early_prev) wx_store(s_excl_last, tot1, tile1, cur ^ 1);  // t_{k-1}, the last tile, resolved early
+      wx_store(s_excl[cur], tot2, tile2, cur);  // t_{k-2} (its offset resolved in iteration k - 1)
     }
     __syncthreads();
     // phase 3: data waves stage t_k into buffer cur; the control wave
     // resolves t_{k-1}'s offset (published one iteration ago)
     if (control) {
-      if (have1 && !early_prev) {
+      if (have1) {
         wx_i64 excl = 0;
 #if WX_DIAG_NO_LOOKBACK  // diagnostic: timing only (results invalid)
         excl = WX_DIAG_NO_LOOKBACK == 2 ? tile1 * WX_TILE * 5 / 8 + 3 : tile1 * WX_TILE / 2;
@@ -1153,20 +1120,6 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
         if (lane == 0) {
           s_excl[cur ^ 1] = excl;  // read when t_{k-1} is written, in iteration k + 1
           if (tile1 == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + tot1;
-        }
-      }
-      if (last_eval) {
-        // this workgroup's last tile: resolve it now too (its aggregate went
-        // out in phase 2), so iteration k + 1 writes t_{k-1} and t_k together
-        // and the drain is one iteration, not two
-        wx_i64 excl = 0;
-        if (tile > 0) {
-          excl = wx_lookback(wx_a, tile);
-          if (lane == 0) wx::st_agent(&wx_a.status[tile], wx_E | WX_FLAG_P | (wx_u64)(excl + block_total));
-        }
-        if (lane == 0) {
-          s_excl_last = excl;
-          if (tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
         }
       }
     } else if (have) {
@@ -1188,8 +1141,6 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
     tile1 = tile;
     tot1 = have ? block_total : 0u;
     tile = next_tile;
-    if (early_prev) break;  // t_{k-1} and t_k written: nothing left
-    early_prev = last_eval;
   }
 #if WX_DIAG_TIMELINE
   if (tid == 0 && wx_a.diag) {

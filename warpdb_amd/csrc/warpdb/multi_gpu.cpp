@@ -292,9 +292,40 @@ void allreduce_f64(const std::vector<ShardRange> &shards, const std::vector<doub
 
 // SUM over shards already in HBM: one reduce per device, then one RCCL
 // all-reduce of {sum (f64), count (i64)} across the shards' devices.
+// Exchange timing of resident-shard queries: an event pair per device and
+// query, recorded on the shard's stream around the collective and the merge.
+struct ExchangeTimer {
+  bool kernels = false, exchange = false;
+  std::vector<std::vector<std::pair<hipEvent_t, hipEvent_t>>> ev;  // [shard][query]
+  std::vector<hipEvent_t> open;                                     // [shard] the pending start event
+  void begin(const std::vector<ShardRange> &ranges, const std::vector<hipStream_t> &streams) {
+    if (!exchange) return;
+    ev.resize(ranges.size());
+    open.assign(ranges.size(), nullptr);
+    for (size_t i = 0; i < ranges.size(); ++i) {
+      DevGuard g(ranges[i].device);
+      hip_ok(hipEventCreateWithFlags(&open[i], hipEventDisableSystemFence), "hipEventCreate");
+      hip_ok(hipEventRecord(open[i], streams[i]), "hipEventRecord");
+    }
+  }
+  void end(const std::vector<ShardRange> &ranges, const std::vector<hipStream_t> &streams) {
+    if (!exchange || open.size() != ranges.size()) return;
+    for (size_t i = 0; i < ranges.size(); ++i) {
+      DevGuard g(ranges[i].device);
+      hipEvent_t e = nullptr;
+      hip_ok(hipEventCreateWithFlags(&e, hipEventDisableSystemFence), "hipEventCreate");
+      hip_ok(hipEventRecord(e, streams[i]), "hipEventRecord");
+      ev[i].push_back({open[i], e});
+    }
+    open.clear();
+  }
+  int32_t flags() const { return kernels ? WX_F_TIME : 0; }
+};
+
 std::pair<double, int64_t> sum_over_shards(const std::vector<ShardRange> &shards, std::vector<Shard> &keep,
                                            const std::string &expr_cuda, const std::string &cond_cuda,
-                                           const HostTable *upload_from, std::vector<DeviceBuffer> *cached = nullptr) {
+                                           const HostTable *upload_from, std::vector<DeviceBuffer> *cached = nullptr,
+                                           ExchangeTimer *timer = nullptr) {
   if (shards.empty()) return {0.0, 0};
   std::vector<DeviceBuffer> local;
   std::vector<DeviceBuffer> &outs = cached ? *cached : local;  // {sum, count} per shard (kept by resident shards)
@@ -309,7 +340,7 @@ std::pair<double, int64_t> sum_over_shards(const std::vector<ShardRange> &shards
     if (!outs[i].ptr) outs[i] = DeviceBuffer(r.device, 16);
     WxTableView v(keep[i].table);
     wx_launch L = sync_launch(r.device, streams[i]);
-    L.flags = WX_F_F64_COUNTS;  // {sum, count} as two doubles; asynchronous until after the collective
+    L.flags = WX_F_F64_COUNTS | (timer ? timer->flags() : 0);  // {sum, count} as two doubles; asynchronous until after the collective
     char err[8192];
     throw_on(wx_reduce_sum(&v.table, expr_cuda.c_str(), cond_cuda.c_str(), &L, outs[i].ptr, nullptr, nullptr, err,
                            sizeof(err)),
@@ -318,7 +349,10 @@ std::pair<double, int64_t> sum_over_shards(const std::vector<ShardRange> &shards
   const int nshard = static_cast<int>(shards.size());
   std::vector<double *> ptrs;
   for (auto &o : outs) ptrs.push_back(static_cast<double *>(o.ptr));
+  const bool coll = nshard > 1 || exchange_one_rank();
+  if (coll && timer) timer->begin(shards, streams);
   allreduce_f64(shards, ptrs, streams, 2);
+  if (coll && timer) timer->end(shards, streams);
   double res[2] = {0, 0};
   for (int i = 0; i < nshard; ++i) {
     DevGuard g(shards[i].device);
@@ -379,6 +413,7 @@ constexpr size_t kTopkRec = kTopkMax * 4 + kTopkMax * 4 + kTopkMax * 8 + 8;  // 
 
 struct ResidentShards::Impl {
   int64_t n = 0;
+  ExchangeTimer timer;
   std::vector<ShardRange> ranges;
   std::vector<Shard> shards;
   std::vector<GroupScratch> group;
@@ -535,6 +570,7 @@ TopkResult ResidentShards::topk_heads(const std::string &order_cuda, const std::
     hip_ok(hipMemcpy(impl_->topk[0].hall.ptr, all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy");
   } else if (ns > 1 || exchange_one_rank()) {
     gathered = true;
+    impl_->timer.begin(ranges, streams);
     Comms &cm = comms_for(static_cast<int>(ns));
     std::lock_guard<std::mutex> clk(cm.mu);
     if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
@@ -609,7 +645,7 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
     char *c = static_cast<char *>(t.cand.ptr);
     WxTableView v(impl_->shards[i].table);
     wx_launch L = sync_launch(r.device, streams[i]);
-    L.flags = 0;  // asynchronous until after the collective
+    L.flags = impl_->timer.flags();  // asynchronous until after the collective
     char err[8192];
     throw_on(wx_topk(&v.table, order_cuda.c_str(), cond_cuda.c_str(), select_cuda.empty() ? nullptr : select_cuda.c_str(),
                      static_cast<int32_t>(k), descending ? 1 : 0, &L, r.begin, reinterpret_cast<float *>(c),
@@ -632,6 +668,7 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
     }
   } else if (ns > 1 || exchange_one_rank()) {
     gathered = true;
+    impl_->timer.begin(ranges, streams);
     Comms &cm = comms_for(static_cast<int>(ns));
     std::lock_guard<std::mutex> clk(cm.mu);
     if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
@@ -664,6 +701,7 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
                            reinterpret_cast<int64_t *>(o + kTopkMax * 16), nullptr, err, sizeof(err)),
              err);
   }
+  impl_->timer.end(ranges, streams);  // no-op unless begin ran (a collective)
   for (size_t i = 0; i < ns; ++i) {
     DevGuard dg(ranges[i].device);
     hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
@@ -685,7 +723,52 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
 
 std::pair<double, int64_t> ResidentShards::sum(const std::string &expr_cuda, const std::string &cond_cuda) const {
   std::lock_guard<std::mutex> lk(impl_->mu);
-  return sum_over_shards(impl_->ranges, impl_->shards, expr_cuda, cond_cuda, nullptr, &impl_->sum_out);
+  return sum_over_shards(impl_->ranges, impl_->shards, expr_cuda, cond_cuda, nullptr, &impl_->sum_out,
+                         &impl_->timer);
+}
+
+void ResidentShards::set_timing(bool kernels, bool exchange) {
+  std::lock_guard<std::mutex> lk(impl_->mu);
+  impl_->timer.kernels = kernels;
+  impl_->timer.exchange = exchange;
+}
+
+ApiTiming ResidentShards::take_timing() {
+  std::lock_guard<std::mutex> lk(impl_->mu);
+  ApiTiming out;
+  for (size_t i = 0; i < impl_->ranges.size(); ++i) {
+    const int dev = impl_->ranges[i].device;
+    bool seen = false;
+    for (size_t j = 0; j < i; ++j) seen = seen || impl_->ranges[j].device == dev;
+    if (seen) continue;  // virtual shards on one device: its launches are read once
+    double ms = 0;
+    int64_t n = 0;
+    char err[1024];
+    throw_on(wx_timing_read_device(dev, &ms, &n, err, sizeof(err)), err);
+    if (n > 0 && ms / n > out.kernel_ms) {
+      out.kernel_ms = ms / n;
+      out.launches = n;
+    }
+  }
+  auto &ev = impl_->timer.ev;
+  for (size_t i = 0; i < ev.size() && i < impl_->ranges.size(); ++i) {
+    DevGuard g(impl_->ranges[i].device);
+    double tot = 0;
+    for (auto &p : ev[i]) {
+      hip_ok(hipEventSynchronize(p.second), "hipEventSynchronize");
+      float ms = 0;
+      hip_ok(hipEventElapsedTime(&ms, p.first, p.second), "hipEventElapsedTime");
+      tot += ms;
+      (void)hipEventDestroy(p.first);
+      (void)hipEventDestroy(p.second);
+    }
+    if (!ev[i].empty()) {
+      out.exchanges = static_cast<int64_t>(ev[i].size());
+      out.exchange_ms = std::max(out.exchange_ms, tot / ev[i].size());
+    }
+    ev[i].clear();
+  }
+  return out;
 }
 
 // GROUP BY over the shards in ONE collective: per device
@@ -728,7 +811,7 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
     }
     WxTableView v(impl_->shards[i].table);
     wx_launch L = sync_launch(r.device, streams[i]);
-    L.flags = 0;  // asynchronous until after the collective
+    L.flags = impl_->timer.flags();  // asynchronous until after the collective
     char err[8192];
     throw_on(wx_group_partials_slots(&v.table, val_cuda.c_str(), key_cuda.c_str(), cond_cuda.c_str(), &L, key_lo,
                                      static_cast<double *>(g.win.ptr), static_cast<int32_t>(ns),
@@ -737,6 +820,8 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
              err);
     wins[i] = static_cast<double *>(g.win.ptr);
   });
+  const bool coll = ns > 1 || exchange_one_rank();
+  if (coll) impl_->timer.begin(ranges, streams);
   allreduce_f64(ranges, wins, streams, WD);
   GroupScratch &g0 = impl_->group[0];
   const int dev0 = ranges[0].device;
@@ -748,6 +833,7 @@ GroupResult ResidentShards::group_sum(const std::string &val_cuda, const std::st
                                   static_cast<int64_t *>(g0.oc.ptr), static_cast<int64_t *>(g0.ng.ptr), nullptr, err,
                                   sizeof(err)),
            err);
+  if (coll) impl_->timer.end(ranges, streams);
   // the group count and the first kStage groups, in one batch of
   // asynchronous copies behind the combine
   constexpr int64_t kStage = 4096;

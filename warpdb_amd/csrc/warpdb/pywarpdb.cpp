@@ -275,7 +275,26 @@ PYBIND11_MODULE(pywarpdb, m) {
           py::arg("order"), py::arg("cond") = "", py::arg("select") = "", py::arg("k") = 5,
           py::arg("descending") = true)
       .def("dense", &warpdb::ResidentShards::dense, py::arg("expr"), py::arg("cond") = "",
-           py::call_guard<py::gil_scoped_release>());
+           py::call_guard<py::gil_scoped_release>())
+      .def("set_timing", &warpdb::ResidentShards::set_timing, py::arg("kernels"), py::arg("exchange") = false,
+           "time the next queries' main kernels (HIP events) and / or their exchanges")
+      .def(
+          "take_timing",
+          [](warpdb::ResidentShards &r) {
+            warpdb::ApiTiming t;
+            {
+              py::gil_scoped_release nogil;
+              t = r.take_timing();
+            }
+            py::dict d;
+            d["kernel_ms"] = t.kernel_ms;
+            d["launches"] = t.launches;
+            d["exchange_ms"] = t.exchange_ms < 0 ? py::object(py::none()) : py::object(py::float_(t.exchange_ms));
+            d["exchanges"] = t.exchanges;
+            return d;
+          },
+          "{kernel_ms: average main-kernel time (slowest device), launches, exchange_ms (None: no collective ran), "
+          "exchanges} since the last read");
 
   m.def(
       "analyze_condition",
