@@ -5,7 +5,7 @@ first (the previous call's range, a sample, or an exact pass): a range that
 fits the 2048-key LDS window moves the window onto it; a range up to 2^24
 keys takes the range-partitioned kernels (tiles sorted in place by partition
 + run directory -> plan -> LDS aggregation per work item -> count -> emit,
-wx_template.hip wx_group_part_*; rows outside a guessed range send the query
+wx_group_part.hip; rows outside a guessed range send the query
 round again over the exact range); wider ranges keep the window + global
 hash.  Every form against the oracle's
 std::map-order double sums (tests/sql_features_test.cpp:14-19 intent): keys

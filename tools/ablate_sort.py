@@ -2,7 +2,7 @@
 """Where a radix pass spends its time (GPU, diagnostic only).
 
 Sorts 1e9 uniform float32 keys with diagnostic builds of the pass kernel
-(WARPDB_EXTRA_DEFINES, see wx_template.hip): without the look-back, without
+(WARPDB_EXTRA_DEFINES, see warpdb_amd/csrc/kernels/wx_radix.hip): without the look-back, without
 the in-wave ranking, without the global key stores, and combinations.  The
 diagnostic builds produce wrong orders; only their times mean anything.
 

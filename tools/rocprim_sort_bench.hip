@@ -1,6 +1,6 @@
 // Baseline for wx_sort_float: rocPRIM's radix_sort_keys (the vendor library
 // sort) on the same 1e9 uniform float32 keys, timed with HIP events.
-// Comparison tool only; the product sort is wx_radix_* (wx_template.hip).
+// Comparison tool only; the product sort is wx_radix_* (warpdb_amd/csrc/kernels/wx_radix.hip).
 #include <hip/hip_runtime.h>
 #include <cstring>
 #include <rocprim/rocprim.hpp>

@@ -1,7 +1,7 @@
 // wx_group_rows.hip -- GROUP BY with every group's sum folded in ascending
 // row order (WX_F_ROW_ORDER): the reference's std::map fold
 // (src/warpdb.cpp:373-385, `g.sum += val` over the rows in order) to the bit.
-// Appended after wx_template.hip to the GROUP and util modules' sources.
+// Part of the GROUP and util modules' sources (after wx_common.hip and their own).
 //
 // When the groups' keys span at most 2048 values (C3's 1K keys), the
 // passing rows' values are put into key-major, row-ordered segments by one

@@ -1,0 +1,802 @@
+// wx_util.hip -- the util module: exchange merges, sort utilities, heads, row-order fold
+// (one of the kernel sources warpexec concatenates after wx_common.hip, whose
+// header describes the prelude they expect)
+
+// ===========================================================================
+#if WX_OP == WX_OP_UTIL
+// Synthetic data generator and the stable sort used by the legacy
+// jit_sort_* entry points (bitonic network over 64-bit (rank << 32 | pos)
+// keys: LDS passes for spans <= 2 * WX_BLOCK * 4, global passes above).
+__device__ __forceinline__ wx_u64 wx_splitmix64(wx_u64 x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_fill_synthetic(WxFillArgs a) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  const float flo = (float)a.lo, fspan = (float)a.hi - (float)a.lo;
+  const wx_i64 ilo = (wx_i64)a.lo, ispan = (wx_i64)a.hi - (wx_i64)a.lo + 1;
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.n; i += stride) {
+    const wx_u64 h = wx_splitmix64((wx_u64)(a.row_base + i) + a.seed * 0xD1B54A32D192ED03ull);
+    double v;
+    if (a.kind == 0) {
+      const float u = (float)(h >> 40) * (1.0f / 16777216.0f);
+      const float m = __fmul_rn(u, fspan);
+      v = (double)__fadd_rn(flo, m);
+    } else {
+      v = (double)(ilo + (wx_i64)((h >> 32) % (wx_u64)ispan));
+    }
+    switch (a.dtype) {
+      case 0: static_cast<int *>(a.out)[i] = (int)v; break;
+      case 1: static_cast<wx_i64 *>(a.out)[i] = (wx_i64)v; break;
+      case 2: static_cast<float *>(a.out)[i] = (float)v; break;
+      default: static_cast<double *>(a.out)[i] = v; break;
+    }
+  }
+}
+
+// Final GROUP BY result of a row-sharded query (query_multi_gpu GROUP BY):
+// the combined exchange window (sums, counts as f64 -- element-wise sums of
+// every shard's wx_group_partials window) and the combined out-of-window
+// groups (ascending keys) merged in ascending key order: the groups below
+// the window, the non-empty window bins, the groups above.  One 1024-thread
+// block, two window bins per thread, ranked by a block scan (as
+// wx_group_finalize).
+#define WX_GCOMB_BLOCK 1024
+static_assert(WX_GROUP_WINDOW == 2 * WX_GCOMB_BLOCK, "two window bins per combine thread");
+// x_keys / x_sums / x_counts: global or LDS (flat pointers)
+__device__ __forceinline__ void wx_group_combine_body(const WxGroupCombineArgs &a, wx_u32 *s_wtot, wx_i64 *s_nlo) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b0 = 2 * tid;
+  const double c0 = a.window[WX_GROUP_WINDOW + b0], c1 = a.window[WX_GROUP_WINDOW + b0 + 1];
+  if (tid == 0) {  // out-of-window groups below the window
+    wx_i64 lo = 0, hi = a.n_extra;
+    while (lo < hi) {
+      const wx_i64 mid = (lo + hi) >> 1;
+      if (a.x_keys[mid] < a.key_lo) lo = mid + 1;
+      else hi = mid;
+    }
+    *s_nlo = lo;
+  }
+  const wx_u32 f = (c0 != 0.0 ? 1u : 0u) + (c1 != 0.0 ? 1u : 0u);
+  wx_u32 incl = f;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const wx_u32 t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_wtot[wave] = incl;
+  __syncthreads();
+  wx_u32 wbase = 0, wsum = 0;
+#pragma unroll
+  for (int w = 0; w < WX_GCOMB_BLOCK / 64; ++w) {
+    const wx_u32 v = s_wtot[w];
+    wbase += (w < wave) ? v : 0u;
+    wsum += v;
+  }
+  const wx_i64 nlo = *s_nlo;
+  wx_i64 pos = nlo + wbase + incl - f;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int b = b0 + h;
+    const double c = h ? c1 : c0;
+    if (c == 0.0) continue;
+    if (pos < a.capacity) {
+      a.out_keys[pos] = a.key_lo + b;
+      a.out_sums[pos] = a.window[b];
+      a.out_counts[pos] = (wx_i64)c;
+    }
+    ++pos;
+  }
+  const wx_i64 above = nlo + wsum;
+  for (wx_i64 i = tid; i < a.n_extra; i += WX_GCOMB_BLOCK) {
+    const wx_i64 p = i < nlo ? i : above + (i - nlo);
+    if (p < a.capacity) {
+      a.out_keys[p] = a.x_keys[i];
+      a.out_sums[p] = a.x_sums[i];
+      a.out_counts[p] = a.x_counts[i];
+    }
+  }
+  if (tid == 0) *a.n_groups_out = above + (a.n_extra - nlo);
+}
+
+extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine(WxGroupCombineArgs a) {
+  __shared__ wx_u32 s_wtot[WX_GCOMB_BLOCK / 64];
+  __shared__ wx_i64 s_nlo;
+  wx_group_combine_body(a, s_wtot, &s_nlo);
+}
+
+// The one-collective form (wx_group_combine_slots): the exchange buffer is
+// the window followed by one slot per shard (count, then (key, sum, count)
+// triples, ascending keys).  The slots' groups are sorted in LDS by (key,
+// slot), groups of equal key are summed in slot order (so every rank and
+// every run adds them in the same order), and the unique groups are merged
+// with the window exactly as wx_group_combine does.  A slot whose shard had
+// more out-of-window groups than fit (count > slot_groups) makes the result
+// -2: the caller merges those groups with a variable-size exchange instead.
+extern "C" __global__ __launch_bounds__(WX_GCOMB_BLOCK) void wx_group_combine_slots(WxGroupSlotsArgs a) {
+  __shared__ wx_u64 s_ent[WX_GROUP_SLOT_MAX];  // (key ^ sign) << 32 | slot-major entry index
+  __shared__ int s_key[WX_GROUP_SLOT_MAX];
+  __shared__ double s_sum[WX_GROUP_SLOT_MAX];
+  __shared__ wx_i64 s_cnt[WX_GROUP_SLOT_MAX];
+  __shared__ int s_off[WX_GCOMB_BLOCK + 1];  // entry offset of each slot (n_slots <= WX_GCOMB_BLOCK)
+  __shared__ wx_u32 s_wtot[WX_GCOMB_BLOCK / 64];
+  __shared__ wx_i64 s_nlo;
+  __shared__ int s_state;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int sl = 1 + 3 * a.slot_groups;
+  const double *slots = a.exchange + WX_GROUP_EXCHANGE;
+  if (tid == 0) s_state = 0;
+  {  // slot counts (thread r: slot r), their prefix by a block scan
+    const double c = tid < a.n_slots ? slots[(wx_i64)tid * sl] : 0.0;
+    __syncthreads();
+    if (c < 0.0) atomicMax(&s_state, 2);
+    else if (c > (double)a.slot_groups) atomicMax(&s_state, 1);
+    const wx_u32 mine = (c > 0.0 && c <= (double)a.slot_groups) ? (wx_u32)c : 0u;
+    wx_u32 incl = mine;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_u32 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_wtot[wave] = incl;
+    __syncthreads();
+    wx_u32 base = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WX_GCOMB_BLOCK / 64; ++w) {
+      const wx_u32 v = s_wtot[w];
+      base += (w < wave) ? v : 0u;
+      tot += v;
+    }
+    s_off[tid] = (int)(base + incl - mine);
+    if (tid == 0) s_off[a.n_slots] = (int)tot;
+    __syncthreads();
+  }
+  if (s_state != 0) {
+    if (tid == 0) *a.n_groups_out = s_state == 2 ? -1 : -2;
+    return;
+  }
+  const int T = s_off[a.n_slots];
+  int npad = 1;
+  while (npad < T) npad <<= 1;
+  for (int i = tid; i < npad; i += WX_GCOMB_BLOCK) {
+    wx_u64 e = ~0ull;
+    if (i < T) {
+      int lo = 0, hi = a.n_slots - 1;  // the slot holding entry i: last r with s_off[r] <= i
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_off[mid] <= i) lo = mid;
+        else hi = mid - 1;
+      }
+      const int j = i - s_off[lo];
+      const int key = (int)slots[(wx_i64)lo * sl + 1 + 3 * j];
+      e = ((wx_u64)((wx_u32)key ^ 0x80000000u) << 32) | ((wx_u32)lo * (wx_u32)a.slot_groups + (wx_u32)j);
+    }
+    s_ent[i] = e;
+  }
+  __syncthreads();
+  for (int k = 2; k <= npad; k <<= 1)
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < npad; i += WX_GCOMB_BLOCK) {
+        const int p = i ^ j;
+        if (p > i) {
+          const wx_u64 x = s_ent[i], y = s_ent[p];
+          const bool up = (i & k) == 0;
+          if ((x > y) == up) { s_ent[i] = y; s_ent[p] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  // unique keys: run heads ranked by a block scan (4 consecutive entries per thread)
+  constexpr int PER = WX_GROUP_SLOT_MAX / WX_GCOMB_BLOCK;
+  wx_u32 hm = 0u, nh = 0u;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int i = tid * PER + q;
+    if (i < T && (i == 0 || (s_ent[i] >> 32) != (s_ent[i - 1] >> 32))) { hm |= 1u << q; ++nh; }
+  }
+  wx_u32 incl = nh;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const wx_u32 t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_wtot[wave] = incl;
+  __syncthreads();
+  wx_u32 wbase = 0, usum = 0;
+#pragma unroll
+  for (int w = 0; w < WX_GCOMB_BLOCK / 64; ++w) {
+    const wx_u32 v = s_wtot[w];
+    wbase += (w < wave) ? v : 0u;
+    usum += v;
+  }
+  wx_u32 u = wbase + incl - nh;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    if (!(hm & (1u << q))) continue;
+    const int i0 = tid * PER + q;
+    const wx_u32 kk = (wx_u32)(s_ent[i0] >> 32);
+    double sum = 0.0;
+    wx_i64 cnt = 0;
+    for (int i = i0; i < T && (wx_u32)(s_ent[i] >> 32) == kk; ++i) {  // slot order
+      const wx_u32 ent = (wx_u32)s_ent[i];
+      const int r = (int)(ent / (wx_u32)a.slot_groups), j = (int)(ent % (wx_u32)a.slot_groups);
+      const double *g = slots + (wx_i64)r * sl + 1 + 3 * j;
+      sum += g[1];
+      cnt += (wx_i64)g[2];
+    }
+    s_key[u] = (int)(kk ^ 0x80000000u);
+    s_sum[u] = sum;
+    s_cnt[u] = cnt;
+    ++u;
+  }
+  __syncthreads();
+  WxGroupCombineArgs c;
+  c.window = a.exchange;
+  c.x_keys = s_key;
+  c.x_sums = s_sum;
+  c.x_counts = s_cnt;
+  c.n_extra = usum;
+  c.key_lo = a.key_lo;
+  c.out_keys = a.out_keys;
+  c.out_sums = a.out_sums;
+  c.out_counts = a.out_counts;
+  c.capacity = a.capacity;
+  c.n_groups_out = a.n_groups_out;
+  wx_group_combine_body(c, s_wtot + 0, &s_nlo);
+}
+
+// Many-key row-sharded GROUP BY (wx_group_merge_lists; replaces a host merge
+// of the shards' groups, src/multi_gpu_utils.cpp:23-60 gathers on the host):
+// every shard's groups arrive as one fixed-size list record (ascending unique
+// keys) from ONE all-gather.  wx_glist_place puts each group at its place in
+// (key, list) order -- its index in its own list plus, per other list, the
+// groups with a smaller key (and, from an earlier list, an equal one), found
+// by binary search -- and marks the first group of each key; wx_glist_count
+// counts those heads per WX_GLIST_SPAN places; wx_glist_scan turns the counts
+// into offsets, places the window's groups and publishes the totals;
+// wx_glist_emit sums each run of equal keys in list order (every rank adds
+// them alike) and writes the unique groups below and above the window's.
+static_assert(WX_GROUP_WINDOW == 2 * WX_GLIST_BLOCK, "two window bins per list-merge thread");
+__device__ __forceinline__ wx_i64 wx_gl_raw(const WxGroupListsArgs &a, int r) {
+  return *reinterpret_cast<const wx_i64 *>(a.lists + (wx_i64)r * a.list_bytes);
+}
+__device__ __forceinline__ wx_i64 wx_gl_valid(const WxGroupListsArgs &a, int r) {  // a bad count reads as empty
+  const wx_i64 c = wx_gl_raw(a, r);
+  return (c < 0 || c > a.list_cap) ? 0 : c;
+}
+__device__ __forceinline__ const int *wx_gl_keys(const WxGroupListsArgs &a, int r) {
+  return reinterpret_cast<const int *>(a.lists + (wx_i64)r * a.list_bytes + 8);
+}
+__device__ __forceinline__ wx_i64 wx_gl_lower(const int *keys, wx_i64 n, int k) {  // keys[0..n) below k
+  wx_i64 lo = 0, hi = n;
+  while (lo < hi) {
+    const wx_i64 mid = (lo + hi) >> 1;
+    if (keys[mid] < k) lo = mid + 1;
+    else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ wx_i64 wx_gl_merged(const WxGroupListsArgs &a) {
+  wx_i64 m = 0;
+  for (int r = 0; r < a.n_lists; ++r) m += wx_gl_valid(a, r);
+  return m;
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_glist_place(WxGroupListsArgs a) {
+  const wx_i64 total = (wx_i64)a.n_lists * a.list_cap;
+  for (wx_i64 q = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; q < total; q += (wx_i64)gridDim.x * WX_BLOCK) {
+    const int r = (int)(q / a.list_cap);
+    const wx_i64 i = q - (wx_i64)r * a.list_cap;
+    if (i >= wx_gl_valid(a, r)) continue;
+    const unsigned char *rec = a.lists + (wx_i64)r * a.list_bytes;
+    const int k = wx_gl_keys(a, r)[i];
+    wx_i64 pos = i;
+    bool head = true;
+    for (int s = 0; s < a.n_lists; ++s) {
+      if (s == r) continue;
+      const int *ks = wx_gl_keys(a, s);
+      const wx_i64 ns = wx_gl_valid(a, s);
+      const wx_i64 lb = wx_gl_lower(ks, ns, k);
+      const bool eq = lb < ns && ks[lb] == k;
+      if (s < r) {
+        pos += lb + (eq ? 1 : 0);
+        head = head && !eq;
+      } else {
+        pos += lb;
+      }
+    }
+    a.m_keys[pos] = k;
+    a.m_sums[pos] = reinterpret_cast<const double *>(rec + a.sums_off)[i];
+    a.m_cnts[pos] = reinterpret_cast<const wx_i64 *>(rec + a.counts_off)[i];
+    a.m_head[pos] = head ? 1u : 0u;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_GLIST_BLOCK) void wx_glist_count(WxGroupListsArgs a) {
+  __shared__ wx_u32 s_w[WX_GLIST_BLOCK / 64];
+  __shared__ wx_i64 s_m;
+  const int tid = threadIdx.x;
+  if (tid == 0) s_m = wx_gl_merged(a);
+  __syncthreads();
+  const wx_i64 m = s_m;
+  const wx_i64 p0 = (wx_i64)blockIdx.x * WX_GLIST_SPAN + (wx_i64)tid * WX_GLIST_PER;
+  wx_u32 c = 0u;
+#pragma unroll
+  for (int j = 0; j < WX_GLIST_PER; ++j)
+    if (p0 + j < m) c += a.m_head[p0 + j];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((tid & 63) == 0) s_w[tid >> 6] = c;
+  __syncthreads();
+  if (tid == 0) {
+    wx_i64 t = 0;
+    for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) t += s_w[w];
+    a.blk[blockIdx.x] = t;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_GLIST_BLOCK) void wx_glist_scan(WxGroupListsArgs a) {
+  __shared__ wx_i64 s_w[WX_GLIST_BLOCK / 64];
+  __shared__ wx_i64 s_carry, s_p0, s_pb;
+  __shared__ int s_bad;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) {
+    s_carry = 0;
+    s_p0 = 0;
+    s_pb = 0;
+    s_bad = 0;
+  }
+  __syncthreads();
+  // list validity, and P0 = groups with a key below the window (their places come first)
+  for (int r = tid; r < a.n_lists; r += WX_GLIST_BLOCK) {
+    const wx_i64 c = wx_gl_raw(a, r);
+    if (c < 0 || c > a.list_cap) atomicOr(&s_bad, 1);
+    if (a.window)
+      atomicAdd(reinterpret_cast<unsigned long long *>(&s_p0),
+                (unsigned long long)wx_gl_lower(wx_gl_keys(a, r), wx_gl_valid(a, r), a.key_lo));
+  }
+  __syncthreads();
+  const wx_i64 p0 = s_p0;
+  const wx_i64 b0 = p0 / WX_GLIST_SPAN;
+  // exclusive prefix of the per-span head counts, 1024 spans per round
+  for (wx_i64 base = 0; base < a.n_blk; base += WX_GLIST_BLOCK) {
+    const wx_i64 i = base + tid;
+    const wx_i64 v = i < a.n_blk ? a.blk[i] : 0;
+    wx_i64 incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_i64 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    wx_i64 wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) {
+      const wx_i64 x = s_w[w];
+      wb += w < wave ? x : 0;
+      tot += x;
+    }
+    const wx_i64 carry = s_carry;
+    if (i < a.n_blk) {
+      a.blk[i] = carry + wb + incl - v;
+      if (i == b0) s_pb = carry + wb + incl - v;
+    }
+    __syncthreads();
+    if (tid == 0) s_carry = carry + tot;
+    __syncthreads();
+  }
+  const wx_i64 U = s_carry;  // unique keys over all lists
+  // unique keys below the window: the heads before place P0
+  wx_i64 nlo = 0;
+  if (a.window) {
+    if (b0 >= a.n_blk) {
+      nlo = U;
+    } else {
+      const wx_i64 q0 = b0 * WX_GLIST_SPAN + (wx_i64)tid * WX_GLIST_PER;
+      wx_u32 c = 0u;
+#pragma unroll
+      for (int j = 0; j < WX_GLIST_PER; ++j)
+        if (q0 + j < p0) c += a.m_head[q0 + j];
+      wx_i64 cc = c;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) cc += __shfl_xor(cc, o);
+      if (lane == 0) s_w[wave] = cc;
+      __syncthreads();
+      nlo = s_pb;
+      for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) nlo += s_w[w];
+      __syncthreads();
+    }
+  }
+  // the window's non-empty bins, in key order, between the groups below and above it
+  wx_i64 wn = 0;
+  if (a.window) {
+    const int b = 2 * tid;
+    const double c0 = a.window[WX_GROUP_WINDOW + b], c1 = a.window[WX_GROUP_WINDOW + b + 1];
+    const wx_u32 f = (c0 != 0.0 ? 1u : 0u) + (c1 != 0.0 ? 1u : 0u);
+    wx_u32 incl = f;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_u32 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    wx_i64 wb = 0;
+#pragma unroll
+    for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) {
+      wb += w < wave ? s_w[w] : 0;
+      wn += s_w[w];
+    }
+    wx_i64 pos = nlo + wb + incl - f;
+    if (!s_bad) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const double c = h ? c1 : c0;
+        if (c == 0.0) continue;
+        if (pos < a.capacity) {
+          a.out_keys[pos] = a.key_lo + b + h;
+          a.out_sums[pos] = a.window[b + h];
+          a.out_counts[pos] = (wx_i64)c;
+        }
+        ++pos;
+      }
+    }
+  }
+  if (tid == 0) {
+    a.meta[0] = wx_gl_merged(a);
+    a.meta[1] = nlo;
+    a.meta[2] = wn;
+    a.meta[3] = s_bad ? -1 : 0;
+    *a.n_groups_out = s_bad ? -1 : U + wn;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_GLIST_BLOCK) void wx_glist_emit(WxGroupListsArgs a) {
+  __shared__ wx_u32 s_w[WX_GLIST_BLOCK / 64];
+  __shared__ wx_i64 s_m;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (a.meta[3] != 0) return;  // a bad list: the scan reported -1, nothing is written
+  if (tid == 0) s_m = a.meta[0];
+  const wx_i64 nlo = a.meta[1], wn = a.meta[2];
+  __syncthreads();
+  const wx_i64 m = s_m;
+  const wx_i64 p0 = (wx_i64)blockIdx.x * WX_GLIST_SPAN + (wx_i64)tid * WX_GLIST_PER;
+  wx_u32 hm = 0u, nh = 0u;
+#pragma unroll
+  for (int j = 0; j < WX_GLIST_PER; ++j)
+    if (p0 + j < m && a.m_head[p0 + j]) {
+      hm |= 1u << j;
+      ++nh;
+    }
+  wx_u32 incl = nh;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const wx_u32 t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  wx_i64 wb = 0;
+#pragma unroll
+  for (int w = 0; w < WX_GLIST_BLOCK / 64; ++w) wb += w < wave ? s_w[w] : 0u;
+  wx_i64 u = a.blk[blockIdx.x] + wb + incl - nh;
+#pragma unroll
+  for (int j = 0; j < WX_GLIST_PER; ++j) {
+    if (!(hm & (1u << j))) continue;
+    const wx_i64 p = p0 + j;
+    const int k = a.m_keys[p];
+    double sum = a.m_sums[p];  // list order: the first list's sum, then the others' added
+    wx_i64 cnt = a.m_cnts[p];
+    for (wx_i64 q = p + 1; q < m && a.m_keys[q] == k; ++q) {
+      sum += a.m_sums[q];
+      cnt += a.m_cnts[q];
+    }
+    const wx_i64 idx = u < nlo ? u : u + wn;
+    if (idx < a.capacity) {
+      a.out_keys[idx] = k;
+      a.out_sums[idx] = sum;
+      a.out_counts[idx] = cnt;
+    }
+    ++u;
+  }
+}
+
+// Global ORDER BY .. LIMIT k of a row-sharded query from every shard's
+// candidates (wx_topk_merge): n_records records of <= k (key, value, row)
+// candidates each.  A candidate's place is the number of candidates that
+// beat it in the total order (better key -- NaN last, -0.0 == +0.0 -- then
+// the smaller row, then the earlier candidate), counted over all of them in
+// LDS; places < k are written.  n_records * k <= WX_TOPK_MERGE_MAX.
+extern "C" __global__ __launch_bounds__(1024) void wx_topk_merge(WxTopkMergeArgs a) {
+  __shared__ wx_u32 s_r[WX_TOPK_MERGE_MAX];
+  __shared__ wx_i64 s_row[WX_TOPK_MERGE_MAX];
+  __shared__ float s_key[WX_TOPK_MERGE_MAX], s_val[WX_TOPK_MERGE_MAX];
+  __shared__ bool s_ok[WX_TOPK_MERGE_MAX];
+  __shared__ int s_tot;
+  const int tid = threadIdx.x;
+  const int nc = a.n_records * a.k;
+  if (tid == 0) s_tot = 0;
+  for (int c = tid; c < nc; c += 1024) {
+    // one round trip: the record's count and the slot's key, value and row
+    // are independent loads (the slot exists whether or not it is used)
+    const int r = c / a.k, j = c - r * a.k;
+    const unsigned char *rec = a.records + (wx_i64)r * WX_TOPK_REC_BYTES;
+    const wx_i64 m = *reinterpret_cast<const wx_i64 *>(rec + WX_TOPK_MAX * 16);
+    const float key = reinterpret_cast<const float *>(rec)[j];
+    const float val = reinterpret_cast<const float *>(rec + WX_TOPK_MAX * 4)[j];
+    const wx_i64 row = reinterpret_cast<const wx_i64 *>(rec + WX_TOPK_MAX * 8)[j];
+    const wx_u32 o = wx::f2ord(key);
+    s_ok[c] = j < m;
+    s_r[c] = (a.descending || o == 0u) ? o : ~o;  // larger is better; NaN (0) worst
+    s_row[c] = row;
+    s_key[c] = key;
+    s_val[c] = val;
+  }
+  __syncthreads();
+  for (int c = tid; c < nc; c += 1024) {
+    if (!s_ok[c]) continue;
+    atomicAdd(&s_tot, 1);
+    const wx_u32 rc = s_r[c];
+    const wx_i64 wc = s_row[c];
+    int place = 0;
+    for (int d = 0; d < nc; ++d) {
+      if (!s_ok[d] || d == c) continue;
+      const wx_u32 rd = s_r[d];
+      const wx_i64 wd = s_row[d];
+      place += (rd > rc || (rd == rc && (wd < wc || (wd == wc && d < c)))) ? 1 : 0;
+    }
+    if (place < a.k) {
+      if (a.out_keys) a.out_keys[place] = s_key[c];
+      if (a.out_vals) a.out_vals[place] = s_val[c];
+      if (a.out_idx) a.out_idx[place] = wc;
+    }
+  }
+  __syncthreads();
+  if (tid == 0 && a.count_out) *a.count_out = s_tot < a.k ? s_tot : a.k;
+}
+
+// Element-wise C conversion between the column types (wx_cast), e.g. the
+// double GROUP BY sums into the float outputs of jit_group_sum.
+template <typename S, typename D>
+__device__ __forceinline__ void wx_cast_loop(const void *src, void *dst, wx_i64 n) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < n; i += stride)
+    static_cast<D *>(dst)[i] = (D) static_cast<const S *>(src)[i];
+}
+template <typename S>
+__device__ __forceinline__ void wx_cast_to(const WxCastArgs &a) {
+  switch (a.dst_dtype) {
+    case 0: wx_cast_loop<S, int>(a.src, a.dst, a.n); break;
+    case 1: wx_cast_loop<S, wx_i64>(a.src, a.dst, a.n); break;
+    case 2: wx_cast_loop<S, float>(a.src, a.dst, a.n); break;
+    default: wx_cast_loop<S, double>(a.src, a.dst, a.n); break;
+  }
+}
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
+  switch (a.src_dtype) {
+    case 0: wx_cast_to<int>(a); break;
+    case 1: wx_cast_to<wx_i64>(a); break;
+    case 2: wx_cast_to<float>(a); break;
+    default: wx_cast_to<double>(a); break;
+  }
+}
+
+// Row-order GROUP BY sums (WX_F_ROW_ORDER, warpexec.cpp do_group_sum_rows):
+// one wave per group.  The wave finds the group's first row in the
+// key-sorted array (lower bound), checks that exactly its count of rows
+// carry the key, and folds their values in ascending row order, one
+// dependent double add per row -- the reference's std::map fold
+// (src/warpdb.cpp:373-385) to the bit.  The lanes stream the group's values
+// (coalesced, WX_FOLD_U chunks of 64 in flight); the chain runs over them in
+// lane order (LDS broadcasts, or v_readlane with WX_FOLD_LDS=0), so every
+// lane holds the same running sum.
+// A chunk past the group's end is padded with +0.0, which leaves any running
+// sum unchanged (the sum starts at +0.0, so it is never -0.0).  1e9 rows x
+// 1024 keys: 11.4 ms through LDS broadcasts (about 11 ns per dependent
+// double add: the chain itself), 12.1 ms with v_readlane per value, 17 ms
+// with every lane widened first and two readlanes per add.
+#ifndef WX_FOLD_U
+#define WX_FOLD_U 8
+#endif
+#ifndef WX_FOLD_LDS
+#define WX_FOLD_LDS 1
+#endif
+extern "C" __global__ __launch_bounds__(64) void wx_group_fold(WxGroupFoldArgs a) {
+  const int lane = threadIdx.x;
+  __shared__ double s_fold[64];
+  for (wx_i64 g = blockIdx.x; g < a.n_groups; g += gridDim.x) {
+    const int key = a.gkeys[g];
+    const wx_i64 c = a.gcounts[g];
+    wx_i64 lo = 0, hi = a.m;
+    while (lo < hi) {
+      const wx_i64 mid = (lo + hi) >> 1;
+      if (a.skeys[mid] < key) lo = mid + 1;
+      else hi = mid;
+    }
+    if (c < 1 || lo + c > a.m || a.skeys[lo + c - 1] != key || (lo + c < a.m && a.skeys[lo + c] == key)) {
+      if (lane == 0) {
+        atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+        a.out_sums[g] = 0.0;
+      }
+      continue;
+    }
+    const float *v = a.svals + lo;
+    double s = 0.0;
+    for (wx_i64 base = 0; base < c; base += 64 * WX_FOLD_U) {
+      wx_u32 x[WX_FOLD_U];
+#pragma unroll
+      for (int u = 0; u < WX_FOLD_U; ++u) {
+        const wx_i64 i = base + u * 64 + lane;
+        x[u] = i < c ? __float_as_uint(v[i]) : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < WX_FOLD_U; ++u) {
+        if (base + u * 64 >= c) break;  // wave-uniform
+#if WX_FOLD_LDS
+        // the wave's 64 values widened into LDS, then read back by every lane
+        // (same address: a broadcast), 16 at a time, ahead of their adds --
+        // only the adds are on the chain, with no SGPR hand-off per value
+        s_fold[lane] = (double)__uint_as_float(x[u]);
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): one wave, LDS in order
+#pragma unroll
+        for (int jb = 0; jb < 64; jb += 16) {
+          double d[16];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) d[q] = s_fold[jb + q];
+#pragma unroll
+          for (int q = 0; q < 16; ++q) s += d[q];
+        }
+#else
+#pragma unroll
+        for (int j = 0; j < 64; ++j) s += (double)__uint_as_float(__builtin_amdgcn_readlane(x[u], j));
+#endif
+      }
+    }
+    if (lane == 0) a.out_sums[g] = s;
+  }
+}
+
+// ORDER BY .. LIMIT heads of any length (the k > 32 form of the top-K
+// record, wx_order_head / wx_head_merge in warpexec.cpp): positions to carry
+// through the stable key sort, then the sorted head gathered into a record;
+// across shards the records' candidates concatenated in record order, sorted
+// the same way, and the global head emitted.
+#define WX_HEAD_KEYS(rec) reinterpret_cast<const float *>((rec) + 8)
+#define WX_HEAD_VALS(rec, cap) reinterpret_cast<const float *>((rec) + 8 + 4 * (cap))
+#define WX_HEAD_ROWS(rec, cap) reinterpret_cast<const wx_i64 *>((rec) + 8 + 8 * (cap))
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_iota(WxHeadArgs a) {
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.n; i += (wx_i64)gridDim.x * WX_BLOCK)
+    a.idx[i] = (wx_u32)i;
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_head_gather(WxHeadArgs a) {
+  const wx_i64 c = *a.count, m = c < a.limit ? c : a.limit;
+  float *k = reinterpret_cast<float *>(a.record + 8);
+  float *v = k + a.cap;
+  wx_i64 *r = reinterpret_cast<wx_i64 *>(a.record + 8 + 8 * a.cap);
+  for (wx_i64 j = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; j < m; j += (wx_i64)gridDim.x * WX_BLOCK) {
+    const wx_u32 p = a.idx[j];
+    k[j] = a.keys[j];
+    v[j] = a.vals ? a.vals[p] : a.keys[j];
+    r[j] = a.row_base + (wx_i64)a.rows[p];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *reinterpret_cast<wx_i64 *>(a.record) = m;
+}
+
+// one workgroup: the records' valid candidates, record after record
+extern "C" __global__ __launch_bounds__(1024) void wx_head_concat(WxHeadArgs a) {
+  __shared__ wx_i64 s_off[1025];
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    wx_i64 o = 0;
+    for (int r = 0; r < a.n_records; ++r) {
+      s_off[r] = o;
+      wx_i64 c = *reinterpret_cast<const wx_i64 *>(a.records + (wx_i64)r * (8 + 16 * a.cap));
+      c = c < 0 ? 0 : (c > a.cap ? a.cap : c);  // a bad count reads as empty / full
+      o += c;
+    }
+    s_off[a.n_records] = o;
+    *a.cat_count = o;
+  }
+  __syncthreads();
+  for (int r = 0; r < a.n_records; ++r) {
+    const unsigned char *rec = a.records + (wx_i64)r * (8 + 16 * a.cap);
+    const wx_i64 o = s_off[r], c = s_off[r + 1] - o;
+    for (wx_i64 j = tid; j < c; j += 1024) {
+      a.cat_keys[o + j] = WX_HEAD_KEYS(rec)[j];
+      a.cat_idx[o + j] = (wx_u32)((wx_i64)r * a.cap + j);
+    }
+  }
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_head_emit(WxHeadArgs a) {
+  const wx_i64 c = *a.count, m = c < a.limit ? c : a.limit;
+  for (wx_i64 j = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; j < m; j += (wx_i64)gridDim.x * WX_BLOCK) {
+    const wx_u32 p = a.idx[j];
+    const wx_i64 r = (wx_i64)p / a.cap, q = (wx_i64)p % a.cap;
+    const unsigned char *rec = a.records + r * (8 + 16 * a.cap);
+    if (a.out_keys) a.out_keys[j] = a.keys[j];
+    if (a.out_vals) a.out_vals[j] = WX_HEAD_VALS(rec, a.cap)[q];
+    if (a.out_rows) a.out_rows[j] = WX_HEAD_ROWS(rec, a.cap)[q];
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0 && a.count_out) *a.count_out = m;
+}
+
+// kind 0: float values, kind 1: int keys.  Descending order inverts the rank
+// but not the position, so equal keys keep their input order (stable).
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_prep(WxSortPrepArgs a) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.npad; i += stride) {
+    wx_u64 e = ~0ull;
+    if (i < a.n) {
+      wx_u32 r;
+      if (a.kind == 0) {
+        const float f = static_cast<const float *>(a.src)[i];
+        r = wx::f2ord(f);
+        if (r == 0u) r = 0xffffffffu;    // NaN sorts last either way
+        else if (!a.ascending) r = ~r;   // 0x007fffff..0x7ffffffe
+      } else {
+        r = (wx_u32)static_cast<const int *>(a.src)[i] ^ 0x80000000u;
+        if (!a.ascending) r = ~r;
+      }
+      e = ((wx_u64)r << 32) | (wx_u32)i;
+    }
+    a.keys[i] = e;
+  }
+}
+
+// LDS bitonic steps on one WX_SORT_LDS-element slice per block: for every
+// stage k in [a.k, a.j] (a.j = kend) run all partner distances below
+// WX_SORT_LDS.  The first launch covers k = 2 .. WX_SORT_LDS; afterwards each
+// larger stage runs its long distances globally and finishes here.
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_bitonic_lds(WxSortPassArgs a) {
+  __shared__ wx_u64 s[WX_SORT_LDS];
+  const wx_i64 base = (wx_i64)blockIdx.x * WX_SORT_LDS;
+  for (int i = threadIdx.x; i < WX_SORT_LDS; i += WX_BLOCK) s[i] = a.keys[base + i];
+  __syncthreads();
+  for (wx_i64 k = a.k; k <= a.j; k <<= 1) {
+    wx_i64 j = k >> 1;
+    if (j >= WX_SORT_LDS) j = WX_SORT_LDS >> 1;
+    for (; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < WX_SORT_LDS; i += WX_BLOCK) {
+        const int p = i ^ (int)j;
+        if (p > i) {
+          const wx_u64 x = s[i], y = s[p];
+          const bool up = ((base + i) & k) == 0;
+          if ((x > y) == up) { s[i] = y; s[p] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < WX_SORT_LDS; i += WX_BLOCK) a.keys[base + i] = s[i];
+}
+
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_bitonic_global(WxSortPassArgs a) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 i = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; i < a.npad; i += stride) {
+    const wx_i64 p = i ^ a.j;
+    if (p > i) {
+      const wx_u64 x = a.keys[i], y = a.keys[p];
+      const bool up = (i & a.k) == 0;
+      if ((x > y) == up) { a.keys[i] = y; a.keys[p] = x; }
+    }
+  }
+}
+
+// Apply the permutation: dst[r] = src[pos(keys[r])] for 4-byte payloads
+// (float values, or int keys plus float values).
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_sort_apply(WxSortApplyArgs a) {
+  const wx_i64 stride = (wx_i64)gridDim.x * WX_BLOCK;
+  for (wx_i64 r = (wx_i64)blockIdx.x * WX_BLOCK + threadIdx.x; r < a.n; r += stride) {
+    const wx_u32 p = (wx_u32)a.keys[r];
+    static_cast<wx_u32 *>(a.dst_a)[r] = static_cast<const wx_u32 *>(a.src_a)[p];
+    if (a.src_v) a.dst_v[r] = a.src_v[p];
+  }
+}
+
+#endif  // WX_OP == WX_OP_UTIL
