@@ -127,3 +127,22 @@ def test_plain_sums_order_free_within_tolerance():
     rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", capacity=4096)
     assert np.array_equal(k, rk) and np.array_equal(c, rc)
     assert np.allclose(s, rs, rtol=1e-12, atol=0)
+
+
+def test_row_order_general_path_keys_with_nan_bit_patterns():
+    """the general row-order path carries each int key's bits
+    through the float-valued compaction (__int_as_float).  Keys whose bits
+    are signalling / quiet NaN patterns, infinities and -0.0 must come back
+    unchanged (the compaction only moves bits).  Keys this far apart (span >
+    2048) take the general path, not the key-span counting scatter."""
+    n = 200_003
+    rng = np.random.default_rng(29)
+    special = np.array([-8388607, -4194305, -4194304, -8388608, 2139095041, 2143289343, 2143289344, 2139095040,
+                        -2147483648, 0, 1, 7], np.int64).astype(np.int32)  # sNaN, qNaN, -inf, +inf, -0.0, ... bits
+    q = special[rng.integers(0, len(special), n)]
+    cols = {"price": spread_values(rng, n), "quantity": q}
+    g, k, s, c = run(cols, None, 4096)
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", capacity=4096)
+    assert g == len(rk) == len(special)
+    assert np.array_equal(k, rk) and np.array_equal(c, rc)
+    assert np.array_equal(bits(s), bits(rs))

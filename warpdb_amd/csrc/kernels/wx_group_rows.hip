@@ -388,7 +388,10 @@ extern "C" __global__ __launch_bounds__(1024) void wx_ro_base(WxRoBaseArgs a) {
 
 // ---------------------------------------------------------------- fold
 // One wave per group g: its rows are values [start, start + count) of the
-// key-major array (start = the counts of the groups before it).  The wave
+// key-major array (start = the counts of the groups before it).  (Measured
+// and dropped: the chunks staged as floats, read a chunk ahead and widened
+// beside each add -- 14.3 vs 12.35 ms per C3 query, the extra v_cvt per value
+// sits on the chain's issue slots; profiles/r05/group_row_order_fold_ab.txt.)  The wave
 // streams them (coalesced); each 64-value chunk is widened into one half of
 // a two-chunk LDS ring one chunk ahead of its adds and read back by every
 // lane (same address: a broadcast), so only the dependent double adds are on
@@ -443,4 +446,5 @@ extern "C" __global__ __launch_bounds__(64) void wx_ro_fold(WxRoFoldArgs a) {
   }
 }
 static_assert(WX_RO_FOLD_AHEAD % 2 == 0, "the fold's ring index needs an even prefetch depth");
+
 #endif  // WX_OP == WX_OP_UTIL
