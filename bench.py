@@ -454,8 +454,8 @@ def main_ranks(args):
         cols[name] = t
     sq = wd.ShardedQuery(wd.Shard(cols, b, n), custom_src=DISCOUNT_SRC, flags=wx.F_TIME)
     query, expr, aux, kname = WORKLOADS[workload]
-    if workload == "project" and os.environ.get("WARPDB_COMPACT_SCHED", "deep") != "deep":
-        kname = "wx_project_compact"
+    if workload == "project" and os.environ.get("WARPDB_COMPACT_SCHED", "deep") == "ticket":
+        kname = "wx_project_compact_ticket"
     counts = torch.zeros(1, dtype=torch.int64, device="cuda")
 
     if workload == "project":

@@ -36,7 +36,6 @@ VARIANTS = {"masked_writes": ("WX_DENSE_BLEND=0", wx.MODE_DENSE), "blend": ("", 
 res = {k: [] for k in VARIANTS}
 def setenv(v):
     os.environ["WARPDB_EXTRA_DEFINES"] = v[0]
-    os.environ["WARPDB_GRID_PER_CU"] = v[2] if len(v) > 2 else "0"
 
 
 for name, v in VARIANTS.items():

@@ -49,13 +49,13 @@ def check():
     return "ok"
 
 
-ENV_KNOBS = ("WARPDB_RS_ITEMS", "WARPDB_RS_BLOCK", "WARPDB_RS_LBW", "WARPDB_RS_PLAIN", "WARPDB_RS_LEAD",
-             "WARPDB_RS_PERSIST")
+ENV_KNOBS = ("WARPDB_RS_PLAIN", "WARPDB_RS_LEAD", "WARPDB_RS_RANK_ATOMIC")
 
 
 def apply(v):
-    """'A=1,WARPDB_RS_ITEMS=16': WARPDB_* items are environment knobs (the
-    host's tile geometry), the rest kernel defines."""
+    """'WX_RS_ITEMS=16,WARPDB_RS_LEAD=0': WARPDB_* items are environment test
+    hooks, the rest kernel defines (WX_RS_BLOCK / WX_RS_ITEMS among them: the
+    host reads the tile geometry back from the define list)."""
     for k in ENV_KNOBS:
         os.environ.pop(k, None)
     defs = []

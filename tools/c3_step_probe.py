@@ -85,7 +85,7 @@ def snapshot():
 with torch.cuda.stream(s):
     ref = snapshot()
 print(f"rows {n}, {ref[0]} groups, world {dist.get_world_size()}, exchange {sq.exchange}, "
-      f"own stream communicator {sq.stream_comm}, time-event fence {os.environ.get('WARPDB_TIME_EVENT_FENCE', '0')}",
+      f"own stream communicator {sq.stream_comm}",
       flush=True)
 for r in range(2):
     run(eager, "eager")

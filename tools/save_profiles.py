@@ -11,7 +11,7 @@ import shutil
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-K = {"project": "wx_project_compact", "sum": "wx_reduce_sum", "group": "wx_group_sum", "topk": "wx_topk_scan", "dense": "wx_project_dense",
+K = {"project": "wx_project_compact_deep", "sum": "wx_reduce_sum", "group": "wx_group_sum", "topk": "wx_topk_scan", "dense": "wx_project_dense",
      "sort": "wx_radix_tile_k_f_a"}
 rnd = sys.argv[1]
 wls = sys.argv[2:] or list(K)

@@ -135,8 +135,6 @@ struct WxGroupArgs {
   wx_u32 *h_max;    // [hcap]
   wx_u32 hmask;     // hcap - 1 (hcap a power of two)
   int key_lo;
-  int fused;           // 1: the last workgroup runs the finalize (`fin`); ctrs[2] counts finished workgroups
-  WxGroupFinArgs fin;  // the finalize's arguments when fused
 };
 
 

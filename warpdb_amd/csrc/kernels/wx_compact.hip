@@ -14,17 +14,14 @@
 // word is its own payload (single agent-scope 8-byte stores and loads), so no
 // fence is needed, and output rows are never read inside the launch.
 //
-// wx_project_compact (default) is a persistent, software-pipelined kernel:
-// WX_DWAVES data waves + 1 control wave per workgroup, one LDS stage buffer.
-// Iteration k: the data waves evaluate tile t_k (loaded one iteration
-// earlier), issue t_{k+1}'s loads and rank t_k; the control wave publishes
-// t_k's aggregate while the data waves write t_{k-1} out of LDS (coalesced,
-// its offset resolved one iteration earlier); then the data waves stage
-// (value, tile-local row) of t_k into LDS and evaluate t_{k+1} while the
-// control wave runs t_k's look-back.  Block b owns tiles b, b + grid, ... so the grid must be
-// co-resident (the host sizes it from the occupancy query).
-// wx_project_compact_ticket takes one tile per workgroup from a ticket
-// counter: no residency assumption, no pipelining.
+// wx_project_compact_deep (default) is a persistent, software-pipelined
+// kernel: WX_DWAVES data waves + 1 control wave per workgroup, two LDS stage
+// buffers, tiles from a ticket counter (described at the kernel).
+// wx_project_compact_ticket takes one tile per workgroup from the same
+// counter: no pipelining (the robust fallback, WARPDB_COMPACT_SCHED=ticket).
+// (A single-buffer persistent kernel, the round-1 default, was measured
+// slower than the deep one and removed in round 5: profiles/r01/
+// ablate_compact_deep.txt.)
 #define WX_GROUPS WX_COMPACT_GROUPS
 #define WX_DWAVES WX_COMPACT_DWAVES             // data waves per workgroup
 #define WX_DTHREADS (WX_DWAVES * 64)
@@ -40,14 +37,6 @@
 __device__ __forceinline__ wx_u64 wx_cflag(wx_u64 w, wx_u64 E) {
   return (w >> WX_EPOCH_SHIFT) == (E >> WX_EPOCH_SHIFT) ? (w >> 56) & 3ull : 0ull;
 }
-#ifndef WX_COMPACT_VSTORE
-#define WX_COMPACT_VSTORE 1  // 16-byte aligned stores for the output runs (2.65 -> 2.47 ms)
-#endif
-#ifndef WX_COMPACT_WHOLE_LOADS
-// unguarded loads when the next tile is whole: measured slower in the same
-// process (2.71 vs 2.47 ms, profiles/r01/ablate_compact_ab.txt), kept off
-#define WX_COMPACT_WHOLE_LOADS 0
-#endif
 #ifndef WX_STALL_TICKS
 // A waiter gives up after this long (s_memrealtime, 100 MHz) without any
 // polled word changing: progress, not poll count, so a query slowed down by
@@ -65,8 +54,6 @@ __device__ __forceinline__ wx_u64 wx_cflag(wx_u64 w, wx_u64 E) {
 #define WX_DECL_TILE_IN(name, T, slot) T wx_in##slot[WX_GROUPS][4];
 #define WX_LOAD_TILE_IN(name, T, slot) \
   ::wx::load4<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4, wx_a.n_rows, wx_in##slot[wx_g]);
-#define WX_LOAD_TILE_FULL(name, T, slot) \
-  ::wx::load4_full<T>(wx_a.col[slot], wx_tb + (wx_i64)wx_g * (WX_DTHREADS * 4) + (wx_i64)wx_dt * 4, wx_in##slot[wx_g]);
 #define WX_BIND_TILE_IN(name, T, slot) const ::wx::reg<T> name{wx_in##slot[wx_g][wx_e]};
 
 // Exclusive prefix of `tile` from its predecessors' status words; one wave.
@@ -153,13 +140,8 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
 // follows every fetch of the launch; the next launch sees it across the
 // kernel boundary.  (acq_rel here is a buffer_wbl2 + buffer_inv at agent
 // scope, a few µs at the end of every launch.)
-#ifndef WX_RETIRE_ACQ_REL
-#define WX_RETIRE_ACQ_REL 0
-#endif
 __device__ __forceinline__ void wx_retire(wx_u64 *ctrs) {
-  const wx_u64 done = WX_RETIRE_ACQ_REL
-                          ? __hip_atomic_fetch_add(&ctrs[2], 1ull, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT)
-                          : __hip_atomic_fetch_add(&ctrs[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const wx_u64 done = __hip_atomic_fetch_add(&ctrs[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (done == (wx_u64)gridDim.x - 1ull) {
     __hip_atomic_store(&ctrs[0], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(&ctrs[2], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -202,256 +184,23 @@ __device__ __forceinline__ void wx_retire(wx_u64 *ctrs) {
     block_total += gsum;                                       \
   }
 
-#ifndef WX_DIAG_PROFILE
-#define WX_DIAG_PROFILE 0  // per-phase time of data wave 0 / the control wave
-#endif
-#if WX_DIAG_PROFILE
-#define WX_PT(slot)                                              \
-  do {                                                          \
-    const wx_u64 wx_now = __builtin_amdgcn_s_memrealtime();     \
-    wx_prof[slot] += wx_now - wx_prof_t;                        \
-    wx_prof_t = wx_now;                                         \
-  } while (0)
-#else
-#define WX_PT(slot) \
-  do {              \
-  } while (0)
-#endif
-#ifndef WX_COMPACT_TICKETS
-// Tiles from an atomic ticket counter (two iterations ahead) instead of the
-// static b, b + grid, ... schedule: a tile is only ever taken by a running
-// workgroup, so the look-back progresses whatever else shares the GPU (the
-// static schedule deadlocked when two processes' compactions overlapped).
-#define WX_COMPACT_TICKETS 1
-#endif
-#ifndef WX_COMPACT_MINBLOCKS
-#define WX_COMPACT_MINBLOCKS 1  // workgroups per CU the register budget must allow
-#endif
-extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx_project_compact(WxCompactArgs wx_a) {
-  const wx_u64 wx_E = (wx_u64)wx_a.epoch << WX_EPOCH_SHIFT;
-  __shared__ wx_u32 s_cnt[WX_DWAVES][WX_GROUPS];
-  __shared__ float s_val[WX_TILE];
-  __shared__ unsigned short s_off[WX_TILE];
-  __shared__ wx_i64 s_excl;
-  __shared__ wx_i64 s_tiles[4];  // ticket ring: slot k & 3 holds iteration k's tile
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool control = wave == WX_DWAVES;
-  const int wx_dt = tid;  // data-thread index (data waves only)
-  const wx_i64 grid = gridDim.x;
-#if WX_COMPACT_TICKETS
-  if (tid == 0) {
-    s_tiles[0] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    s_tiles[1] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  wx_i64 tile = s_tiles[0];
-#else
-  wx_i64 tile = blockIdx.x;
-#endif
-  wx_i64 prev_tile = -1;
-  WX_COLS(WX_DECL_TILE_IN)
-  if (!control && tile < wx_a.n_tiles) {
-    const wx_i64 wx_tb = tile * WX_TILE;
-#pragma unroll
-    for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
-  }
-  wx_u32 prev_total = 0;
-#if WX_DIAG_PROFILE
-  wx_u64 wx_prof[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  wx_u64 wx_prof_t = __builtin_amdgcn_s_memrealtime();
-#endif
-  for (int k = 0;; ++k) {
-    const bool have = tile < wx_a.n_tiles;
-    const bool have_prev = k > 0 && prev_tile < wx_a.n_tiles;
-    if (!have && !have_prev) break;
-#if WX_COMPACT_TICKETS
-    const wx_i64 next_tile = s_tiles[(k + 1) & 3];  // fetched two iterations ahead
-#else
-    const wx_i64 next_tile = tile + grid;
-#endif
-    const wx_i64 tile_base = tile * WX_TILE;
-    wx_u32 wx_kb = 0;  // bit 4g + e: row (g, e) passes (a VGPR, not 16 SGPR-pair lane masks)
-    float wx_val[WX_GROUPS][4];
-    wx_u32 lane_pre[WX_GROUPS];
-    // phase 1 (data): evaluate t_k, issue t_{k+1}'s loads, rank t_k
-    // (issuing each group's loads right after its evaluation measured slower:
-    // 2.72 vs 2.53 ms, profiles/r01/ablate_compact_interleave.txt)
-    if (!control && have) {
-      // rows of this tile inside the table (workgroup-uniform, 32-bit)
-      const wx_u32 wx_rows = (wx_u32)(wx_a.n_rows - tile_base < WX_TILE ? wx_a.n_rows - tile_base : WX_TILE);
-#pragma unroll
-      for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) {
-#pragma unroll
-        for (int wx_e = 0; wx_e < 4; ++wx_e) {
-          WX_COLS(WX_BIND_TILE_IN)
-          const wx_u32 wx_lrow = (wx_u32)(wx_g * (WX_DTHREADS * 4) + wx_dt * 4 + wx_e);
-          const wx_i64 idx = tile_base + wx_lrow;  // dead unless the expression names idx
-          (void)idx;
-          bool wx_k = wx_lrow < wx_rows;
-          wx_k = wx_k && WX_EVAL_COND();
-          wx_kb |= (wx_k ? 1u : 0u) << (wx_g * 4 + wx_e);
-          wx_val[wx_g][wx_e] = static_cast<float>(WX_EXPR);
-        }
-      }
-      WX_PT(0);  // evaluation, including the wait for t_k's loads
-      const wx_i64 next = next_tile;
-      const wx_i64 wx_tb = next * WX_TILE;
-      if (WX_COMPACT_WHOLE_LOADS && WX_ALIGNED16 && wx_tb + WX_TILE <= wx_a.n_rows) {  // workgroup-uniform
-#pragma unroll
-        for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_FULL) }
-      } else if (next < wx_a.n_tiles) {
-#pragma unroll
-        for (int wx_g = 0; wx_g < WX_GROUPS; ++wx_g) { WX_COLS(WX_LOAD_TILE_IN) }
-      }
-#pragma unroll
-      for (int g = 0; g < WX_GROUPS; ++g) {
-        wx_u32 pre = 0, tot = 0;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const wx_u64 m = __builtin_amdgcn_ballot_w64(((wx_kb >> (g * 4 + e)) & 1u) != 0u);
-          pre += wx::lanes_below(m);
-          tot += (wx_u32)__builtin_popcountll(m);
-        }
-        lane_pre[g] = pre;
-        if (lane == 0) s_cnt[wave][g] = tot;
-      }
-      WX_PT(1);  // issue t_{k+1} loads + rank
-    }
-    __syncthreads();
-    WX_PT(2);  // barrier 1
-    // phase 2: control publishes t_k's aggregate; data waves write t_{k-1} out of LDS
-    wx_u32 block_total = 0;
-    wx_u32 grp_base[WX_GROUPS];
-    if (have) { WX_BASES(s_cnt) }
-    if (control) {
-      if (have && lane == 0)
-        wx::st_agent(&wx_a.status[tile], wx_E | (tile == 0 ? WX_FLAG_P : WX_FLAG_A) | (wx_u64)block_total);
-#if WX_COMPACT_TICKETS
-      // the tile of iteration k + 2 (slot last read as `prev` in iteration k - 1)
-      if (lane == 0)
-        s_tiles[(k + 2) & 3] = next_tile < wx_a.n_tiles
-                                   ? (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED,
-                                                                    __HIP_MEMORY_SCOPE_AGENT)
-                                   : wx_a.n_tiles;  // past the end: stop taking tickets
-#endif
-    } else if (have_prev) {
-      const wx_i64 excl = s_excl;
-      const wx_i64 prev_base = wx_a.row_base + prev_tile * WX_TILE;
-#if !WX_DIAG_NO_STORE
-      // The tile's output run [excl, excl + total): a scalar head up to the
-      // next 32-element boundary (128 B of f32 / i32), aligned 16-byte stores
-      // of four outputs per lane, a scalar tail of < 4.  For this kernel's
-      // 8 B read + 5 B write mix the probe gives 6.2 TB/s with aligned 16-B
-      // stores (r2wt) against 5.1-5.4 with 4-B stores (r2wd4) and 3.6 with
-      // 4-B stores off a 16-B boundary (tools/bw_probe.hip).
-      const wx_i64 end = excl + (wx_i64)prev_total;
-      wx_i64 b0 = WX_COMPACT_VSTORE ? (excl + 31) & ~(wx_i64)31 : end;
-      if (b0 > end) b0 = end;
-      const wx_i64 b1 = b0 + ((end - b0) & ~(wx_i64)3);
-      const int n_head = (int)(b0 - excl), n_edge = n_head + (int)(end - b1);
-      for (int j = wx_dt; j < n_edge; j += WX_DTHREADS) {
-        const wx_i64 pos = j < n_head ? excl + j : b1 + (j - n_head);
-        const int i = (int)(pos - excl);
-        if (wx_a.out_val) wx_a.out_val[pos] = s_val[i];
-        if (wx_a.out_idx) {
-          const wx_i64 gi = prev_base + s_off[i];
-          if (wx_a.idx64) static_cast<wx_i64 *>(wx_a.out_idx)[pos] = gi;
-          else static_cast<int *>(wx_a.out_idx)[pos] = (int)gi;
-        }
-      }
-      for (wx_i64 q = b0 + 4 * (wx_i64)wx_dt; q < b1; q += 4 * (wx_i64)WX_DTHREADS) {
-        const int i = (int)(q - excl);
-        if (wx_a.out_val) {
-          typedef float v4f __attribute__((ext_vector_type(4)));
-          const v4f v = {s_val[i], s_val[i + 1], s_val[i + 2], s_val[i + 3]};
-          wx::stv(reinterpret_cast<v4f *>(wx_a.out_val + q), v);
-        }
-        if (wx_a.out_idx) {
-          if (wx_a.idx64) {
-            typedef long long v2l __attribute__((ext_vector_type(2)));
-            wx_i64 *o = static_cast<wx_i64 *>(wx_a.out_idx) + q;
-            const v2l x = {(long long)(prev_base + s_off[i]), (long long)(prev_base + s_off[i + 1])};
-            const v2l y = {(long long)(prev_base + s_off[i + 2]), (long long)(prev_base + s_off[i + 3])};
-            wx::stv(reinterpret_cast<v2l *>(o), x);
-            wx::stv(reinterpret_cast<v2l *>(o + 2), y);
-          } else {
-            typedef int v4i __attribute__((ext_vector_type(4)));
-            const unsigned base = (unsigned)prev_base;  // int32 indices: (int)(row) as the scalar path
-            const v4i x = {(int)(base + s_off[i]), (int)(base + s_off[i + 1]), (int)(base + s_off[i + 2]),
-                           (int)(base + s_off[i + 3])};
-            wx::stv(reinterpret_cast<v4i *>(static_cast<int *>(wx_a.out_idx) + q), x);
-          }
-        }
-      }
-#else
-      if (excl == -1 && wx_a.out_val) wx_a.out_val[0] = s_val[wx_dt];
-#endif
-    }
-    WX_PT(3);  // data: stores of t_{k-1}; control: publish
-    __syncthreads();
-    WX_PT(4);  // barrier 2
-    // phase 3: data waves stage t_k; the control wave resolves t_k's offset
-    // (overlapping the staging and phase 1 of the next iteration)
-    if (control) {
-      if (have) {
-        wx_i64 excl = 0;
-#if WX_DIAG_NO_LOOKBACK
-        excl = WX_DIAG_NO_LOOKBACK == 2 ? tile_base * 5 / 8 + 3 : tile_base / 2;  // diagnostic: timing only
-#else
-        if (tile > 0) {
-          excl = wx_lookback(wx_a, tile);
-          if (lane == 0) wx::st_agent(&wx_a.status[tile], wx_E | WX_FLAG_P | (wx_u64)(excl + block_total));
-        }
-#endif
-        if (lane == 0) {
-          s_excl = excl;
-          if (tile == wx_a.n_tiles - 1 && wx_a.count_out) *wx_a.count_out = excl + block_total;
-        }
-      }
-    } else if (have) {
-#pragma unroll
-      for (int g = 0; g < WX_GROUPS; ++g) {
-        wx_u32 pos = grp_base[g] + lane_pre[g];
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          if ((wx_kb >> (g * 4 + e)) & 1u) {
-            s_val[pos] = wx_val[g][e];
-            s_off[pos] = (unsigned short)(g * (WX_DTHREADS * 4) + wx_dt * 4 + e);
-            ++pos;
-          }
-        }
-      }
-    }
-    WX_PT(5);  // data: LDS staging of t_k; control: look-back
-    prev_total = block_total;
-    prev_tile = tile;
-    tile = next_tile;
-  }
-  if (tid == 0) wx_retire(wx_a.ctrs);
-#if WX_DIAG_PROFILE
-  if (wx_a.diag && (tid == 0 || tid == WX_DTHREADS)) {
-    wx_u64 *d = wx_a.diag + (wx_u64)blockIdx.x * 16 + (tid == 0 ? 0 : 8);
-    for (int i = 0; i < 6; ++i) d[i] = wx_prof[i];
-  }
-#endif
-}
 
-// Deeper pipeline (WARPDB_COMPACT_SCHED=deep): tile t_j is evaluated and
-// staged in iteration j, its offset resolved by the control wave in
-// iteration j + 1 (its predecessors' aggregates have long landed), and its
-// output written in iteration j + 2 — the look-back gets a whole iteration
-// of slack instead of half of one.  Two stage buffers (2 x 6 B per tile row),
-// so only compiled when selected.  Its output runs leave with nontemporal
-// stores: 2.23 vs 2.29 ms per 1e9 rows in one process
-// (profiles/r01/ablate_compact_deep_nt.txt; the single-buffer kernel was
-// slower with them, ablate_compact_nt.txt).
+// The pipelined compaction.  Iteration k: the data waves evaluate tile t_k
+// (loaded one iteration earlier), issue t_{k+1}'s loads and rank t_k; the
+// control wave publishes t_k's aggregate and takes the ticket of iteration
+// k + 2 while the data waves write t_{k-2} out of LDS (coalesced, its offset
+// resolved one iteration earlier); then the data waves stage (value,
+// tile-local row) of t_k while the control wave resolves t_{k-1}'s offset —
+// the look-back gets a whole iteration of slack.  Two stage buffers
+// (2 x 6 B per tile row).  Any grid size is correct: a workgroup that starts
+// late finds the tickets taken and exits.  Output runs: a scalar head up to
+// the next 32-element boundary (128 B), aligned 16-byte stores of four
+// outputs per lane (2.65 -> 2.47 ms against 4-byte stores,
+// tools/bw_probe.hip), a scalar tail of < 4, all nontemporal: 2.23 vs
+// 2.29 ms per 1e9 rows (profiles/r01/ablate_compact_deep_nt.txt).
 #ifndef WX_DEEP_NT_STORE
 #define WX_DEEP_NT_STORE 1
 #endif
-#ifndef WX_TICKET_PAIR
-#define WX_TICKET_PAIR 1
-#endif
-#if defined(WX_COMPACT_STATIC) && WX_COMPACT_STATIC == 3
 // (Measured and dropped, round 4, profiles/r04/: half-height tiles for each
 // workgroup's last iterations, +2 us per extra tile at 1e8 rows,
 // abl_compact_half_tail.txt; resolving a workgroup's last tile in the
@@ -461,7 +210,7 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #ifndef WX_DIAG_TIMELINE
 #define WX_DIAG_TIMELINE 0  // diagnostic: per-workgroup entry / first-tile / loop-end times (diag[b * 16 ..])
 #endif
-extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx_project_compact_deep(WxCompactArgs wx_a) {
+extern "C" __global__ __launch_bounds__(WX_CBLOCK, 1) void wx_project_compact_deep(WxCompactArgs wx_a) {
   const wx_u64 wx_E = (wx_u64)wx_a.epoch << WX_EPOCH_SHIFT;
 #if WX_DIAG_TIMELINE
   const wx_u64 wx_t_entry = __builtin_amdgcn_s_memrealtime();
@@ -477,14 +226,10 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
   const bool control = wave == WX_DWAVES;
   const int wx_dt = tid;
   if (tid == 0) {
-    if (WX_TICKET_PAIR) {  // one dequeue for both first tiles (the counter word serialises every dequeue)
-      const wx_i64 t0 = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_tiles[0] = t0;
-      s_tiles[1] = t0 + 1;
-    } else {
-      s_tiles[0] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_tiles[1] = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    // one dequeue for both first tiles (the counter word serialises every dequeue)
+    const wx_i64 t0 = (wx_i64)__hip_atomic_fetch_add(&wx_a.ctrs[0], 2ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    s_tiles[0] = t0;
+    s_tiles[1] = t0 + 1;
   }
   __syncthreads();
 #if WX_DIAG_TIMELINE
@@ -668,7 +413,6 @@ extern "C" __global__ __launch_bounds__(WX_CBLOCK, WX_COMPACT_MINBLOCKS) void wx
 #endif
   if (tid == 0) wx_retire(wx_a.ctrs);
 }
-#endif
 
 // One tile per workgroup, taken from a ticket counter (robust fallback).
 extern "C" __global__ __launch_bounds__(WX_DTHREADS) void wx_project_compact_ticket(WxCompactArgs wx_a) {

@@ -29,24 +29,6 @@ __device__ __forceinline__ float wx_mm_out(wx_u32 m, bool is_min) {
   return (is_min ? m == 0xffffffffu : m == 0u) ? __uint_as_float(0x7fc00000u) : wx::ord2f(m);
 }
 
-// Accumulator reads of the finalize: plain across a kernel boundary, agent
-// scope (past the non-coherent L2 of another XCD) inside the launch that wrote them
-template <bool COH>
-__device__ __forceinline__ wx_u64 wx_gld(const wx_u64 *p) {
-  return COH ? wx::ld_agent(p) : *p;
-}
-template <bool COH>
-__device__ __forceinline__ double wx_gldd(const double *p) {
-  return COH ? __longlong_as_double((long long)wx::ld_agent(reinterpret_cast<const wx_u64 *>(p))) : *p;
-}
-template <bool COH>
-__device__ __forceinline__ wx_u32 wx_gld32(const wx_u32 *p) {
-  return COH ? __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : *p;
-}
-template <int NT, bool COH>
-__device__ __forceinline__ void wx_group_finalize_body(const WxGroupFinArgs &a, wx_u64 *s_ent, wx_u32 *s_wtot,
-                                                       wx_i64 &s_nlo);
-
 __device__ __forceinline__ void wx_hash_add(const WxGroupArgs &a, int key, double v, wx_u32 o) {
   const wx_u64 tag = (wx_u64)(wx_u32)key | (1ull << 32);
   wx_u32 h = ((wx_u32)key * 2654435761u) & a.hmask;
@@ -56,8 +38,7 @@ __device__ __forceinline__ void wx_hash_add(const WxGroupArgs &a, int key, doubl
       const wx_u64 prev = atomicCAS(&a.h_tag[h], 0ull, tag);
       if (prev == 0ull) {
         const wx_u64 u = __hip_atomic_fetch_add(&a.ctrs[0], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        // agent scope: a fused finalize in another XCD's workgroup reads it in this launch
-        __hip_atomic_store(&a.h_used[u], h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a.h_used[u] = h;
         cur = tag;
       } else {
         cur = prev;
@@ -84,25 +65,12 @@ __device__ __forceinline__ void wx_hash_add(const WxGroupArgs &a, int key, doubl
 // workgroups flush less for the same waves per CU.
 #undef WX_LBLOCK
 #define WX_LBLOCK WX_GBLOCK
-#ifndef WX_GROUP_FUSED_FIN
-// 1: the last workgroup to finish runs the finalize itself (no second launch
-// and no launch gap) when the host asks for it (wx_a.fused: no device-wide
-// key sort can be needed, capacity <= WX_GROUP_HSORT_MAX)
-#define WX_GROUP_FUSED_FIN (!WX_MINMAX)
-#endif
+// (A finalize fused into the last workgroup to finish, saving the second
+// launch, was measured slower and removed in round 5: 154.8 vs 148.1 us per
+// 1.25e8 rows, profiles/r03/s2/bench_*fused*.json.)
 extern "C" __global__ __launch_bounds__(WX_GBLOCK) void wx_group_sum(WxGroupArgs wx_a) {
-#if WX_GROUP_FUSED_FIN
-  // the window during the scan, the finalize's key sort after the flush
-  __shared__ wx_u64 wx_s_raw[WX_HSORT_MAX > (WX_GWIN * 12 + 7) / 8 ? WX_HSORT_MAX : (WX_GWIN * 12 + 7) / 8];
-  double *wx_s_sum = reinterpret_cast<double *>(wx_s_raw);
-  wx_u32 *wx_s_cnt = reinterpret_cast<wx_u32 *>(wx_s_sum + WX_GWIN);
-  __shared__ wx_u32 wx_s_wtot[WX_GBLOCK / 64];
-  __shared__ wx_i64 wx_s_nlo;
-  __shared__ int wx_s_last;
-#else
   __shared__ double wx_s_sum[WX_GWIN];
   __shared__ wx_u32 wx_s_cnt[WX_GWIN];
-#endif
 #if WX_MINMAX
   __shared__ wx_u32 wx_s_min[WX_GWIN], wx_s_max[WX_GWIN];
 #endif
@@ -152,21 +120,6 @@ extern "C" __global__ __launch_bounds__(WX_GBLOCK) void wx_group_sum(WxGroupArgs
 #endif
     }
   }
-#if WX_GROUP_FUSED_FIN
-  if (!wx_a.fused) return;
-  // this workgroup's flush and hash atomics performed, then its count: the
-  // workgroup that counts last sees every other one's accumulators
-  __builtin_amdgcn_s_waitcnt(0);
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    const wx_u64 done = __hip_atomic_fetch_add(&wx_a.ctrs[2], 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    wx_s_last = done == (wx_u64)gridDim.x - 1ull;
-    if (wx_s_last) __hip_atomic_store(&wx_a.ctrs[2], 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  if (!wx_s_last) return;
-  wx_group_finalize_body<WX_GBLOCK, true>(wx_a.fin, wx_s_raw, wx_s_wtot, wx_s_nlo);
-#endif
 }
 
 #undef WX_LBLOCK
@@ -190,17 +143,16 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_group_gather(WxGroupGa
   }
 }
 
-// The finalize on NT threads: the 1024-thread kernel below, or (COH) the last
-// workgroup of wx_group_sum itself, which reads the accumulators the other
-// workgroups' atomics left with agent-scope loads.  s_ent: WX_HSORT_MAX
-// entries ((key ^ sign) << 32 | used-list position), s_wtot: NT / 64 words.
-template <int NT, bool COH>
+// The finalize on NT threads (the 1024-thread kernel below).  s_ent:
+// WX_HSORT_MAX entries ((key ^ sign) << 32 | used-list position), s_wtot:
+// NT / 64 words.
+template <int NT>
 __device__ __forceinline__ void wx_group_finalize_body(const WxGroupFinArgs &a, wx_u64 *s_ent, wx_u32 *s_wtot,
                                                        wx_i64 &s_nlo) {
   constexpr int BPT = WX_GWIN / NT;  // window bins per thread
   static_assert(WX_GWIN == BPT * NT, "the window divides over the threads");
   const int tid = threadIdx.x;
-  const wx_i64 n_hash = (wx_i64)wx_gld<COH>(&a.ctrs[0]);
+  const wx_i64 n_hash = (wx_i64)a.ctrs[0];
   const bool presorted = a.sorted != nullptr;
   const bool too_many = n_hash > WX_HSORT_MAX && !presorted;
   if (too_many) {
@@ -214,12 +166,12 @@ __device__ __forceinline__ void wx_group_finalize_body(const WxGroupFinArgs &a, 
   const int b0 = tid * BPT;
   wx_u64 wc[BPT];
 #pragma unroll
-  for (int h = 0; h < BPT; ++h) wc[h] = wx_gld<COH>(&a.win_cnt[b0 + h]);
+  for (int h = 0; h < BPT; ++h) wc[h] = a.win_cnt[b0 + h];
   for (int i = tid; !presorted && i < npad; i += NT) {
     wx_u64 e = ~0ull;
     if (i < nh) {
-      const wx_u32 slot = wx_gld32<COH>(&a.h_used[i]);
-      const wx_u32 key = (wx_u32)wx_gld<COH>(&a.h_tag[slot]);
+      const wx_u32 slot = a.h_used[i];
+      const wx_u32 key = (wx_u32)a.h_tag[slot];
       e = ((wx_u64)(key ^ 0x80000000u) << 32) | (wx_u32)i;
     }
     s_ent[i] = e;
@@ -279,7 +231,7 @@ __device__ __forceinline__ void wx_group_finalize_body(const WxGroupFinArgs &a, 
       const int b = b0 + h;
       const wx_u64 c = wc[h];
       if (part) {
-        a.win_out[b] = c ? wx_gldd<COH>(&a.win_sum[b]) : 0.0;
+        a.win_out[b] = c ? a.win_sum[b] : 0.0;
         a.win_out[WX_GWIN + b] = (double)c;
         if (!c) continue;
         a.win_sum[b] = 0.0;
@@ -289,7 +241,7 @@ __device__ __forceinline__ void wx_group_finalize_body(const WxGroupFinArgs &a, 
       if (!c) continue;
       if (pos < a.capacity) {
         a.out_keys[pos] = a.key_lo + b;
-        a.out_sums[pos] = wx_gldd<COH>(&a.win_sum[b]);
+        a.out_sums[pos] = a.win_sum[b];
         a.out_counts[pos] = (wx_i64)c;
 #if WX_MINMAX
         if (a.out_mins) a.out_mins[pos] = wx_mm_out(a.win_min[b], true);
@@ -309,12 +261,12 @@ __device__ __forceinline__ void wx_group_finalize_body(const WxGroupFinArgs &a, 
   // hash entries: below-window ones first, the rest after the window
   for (wx_i64 i = tid; i < nh; i += NT) {
     const wx_u64 e = WX_ENT(i);
-    const wx_u32 slot = wx_gld32<COH>(&a.h_used[(wx_u32)e]);
+    const wx_u32 slot = a.h_used[(wx_u32)e];
     const wx_i64 pos = (i < nlo) ? i : out_pos + (i - nlo);
     if (pos < a.capacity) {
       a.out_keys[pos] = (int)((wx_u32)(e >> 32) ^ 0x80000000u);
-      a.out_sums[pos] = wx_gldd<COH>(&a.h_sum[slot]);
-      a.out_counts[pos] = (wx_i64)wx_gld<COH>(&a.h_cnt[slot]);
+      a.out_sums[pos] = a.h_sum[slot];
+      a.out_counts[pos] = (wx_i64)a.h_cnt[slot];
 #if WX_MINMAX
       if (a.out_mins) a.out_mins[pos] = wx_mm_out(a.h_min[slot], true);
       if (a.out_maxs) a.out_maxs[pos] = wx_mm_out(a.h_max[slot], false);
@@ -339,9 +291,9 @@ __device__ __forceinline__ void wx_group_finalize_body(const WxGroupFinArgs &a, 
           const int j = (o - 1) / 3, fld = (o - 1) - 3 * j;
           if (j < nh) {
             const wx_u64 e = WX_ENT(j);
-            const wx_u32 slot = wx_gld32<COH>(&a.h_used[(wx_u32)e]);
+            const wx_u32 slot = a.h_used[(wx_u32)e];
             v = fld == 0 ? (double)(int)((wx_u32)(e >> 32) ^ 0x80000000u)
-                         : (fld == 1 ? wx_gldd<COH>(&a.h_sum[slot]) : (double)wx_gld<COH>(&a.h_cnt[slot]));
+                         : (fld == 1 ? a.h_sum[slot] : (double)a.h_cnt[slot]);
           }
         }
       }
@@ -352,7 +304,7 @@ __device__ __forceinline__ void wx_group_finalize_body(const WxGroupFinArgs &a, 
   const wx_i64 total = out_pos + (nh - nlo);
   // return the general-key table to its clean state
   for (wx_i64 i = tid; i < n_hash; i += NT) {
-    const wx_u32 slot = wx_gld32<COH>(&a.h_used[i]);
+    const wx_u32 slot = a.h_used[i];
     a.h_tag[slot] = 0ull;
     a.h_sum[slot] = 0.0;
     a.h_cnt[slot] = 0ull;
@@ -374,6 +326,6 @@ extern "C" __global__ __launch_bounds__(WX_GFIN_BLOCK) void wx_group_finalize(Wx
   __shared__ wx_u64 s_ent[WX_HSORT_MAX];  // (key ^ sign) << 32 | used-list position
   __shared__ wx_u32 s_wtot[WX_GFIN_BLOCK / 64];
   __shared__ wx_i64 s_nlo;
-  wx_group_finalize_body<WX_GFIN_BLOCK, false>(a, s_ent, s_wtot, s_nlo);
+  wx_group_finalize_body<WX_GFIN_BLOCK>(a, s_ent, s_wtot, s_nlo);
 }
 #endif

@@ -64,39 +64,12 @@ __device__ __forceinline__ wx_u32 wx_rs_key_t(wx_u32 x) {
   return ASC ? r : ~r;
 }
 
-#ifndef WX_RS_HCOPIES
-#define WX_RS_HCOPIES 8  // LDS histogram copies, picked by lane % copies: few-valued digits conflict 8x less
-#endif
 #ifndef WX_RS_HUNROLL
 #define WX_RS_HUNROLL 4  // 16-byte loads in flight per thread (64 B): the kernel is latency-bound below that
 #endif
-template <int KIND, bool ASC>
-__device__ __forceinline__ void wx_rs_count(wx_u32 *h, wx_u32 x, int lane, int copy) {
-  const wx_u32 k = wx_rs_key_t<KIND, ASC>(x);
-  const wx_u64 act = __builtin_amdgcn_ballot_w64(true);
-  const int first = __builtin_ctzll(act);
-#pragma unroll
-  for (int p = 0; p < 4; ++p) {
-    const wx_u32 d = (k >> (8 * p)) & 255u;
-    const wx_u32 d0 = __builtin_amdgcn_readfirstlane(d);
-    // (Aggregating the first lane's digit group on every wave, not only on a
-    // wave-uniform digit, did not pay: as a second LDS add 18.6 vs 17.7 ms
-    // per 1e9 keys, folded into the lane's own add 17.5 vs 17.5.)
-    if (__builtin_amdgcn_ballot_w64(d != d0) == 0ull) {
-      if (lane == first) atomicAdd(&h[(p * 256 + d0) * WX_RS_HCOPIES], (wx_u32)__builtin_popcountll(act));
-    } else {
-      atomicAdd(&h[(p * 256 + d) * WX_RS_HCOPIES + copy], 1u);
-    }
-  }
-}
-
-#ifndef WX_RS_HWIDE
-#define WX_RS_HWIDE 1  // 1.30 -> 0.66 ms per 1e9 keys with the unconditional, pipelined loads (abl_sort_hwide*.txt)
-#endif
-#ifndef WX_RS_HPIPE
-#define WX_RS_HPIPE 1
-#endif
-#if WX_RS_HWIDE
+// (Round 1's 256-thread histogram with 8 counter copies, 1.30 ms per 1e9
+// keys against this kernel's 0.66, profiles/r02/abl_sort_hwide*.txt, was
+// removed in round 5.)
 // One 1024-thread workgroup per CU with 32 copies of every counter (128 KB):
 // lane l adds to copy l % 32, so the 32 lanes of an LDS cycle always hit 32
 // different banks and never one address -- no digit distribution conflicts.
@@ -111,11 +84,6 @@ __device__ __forceinline__ wx_u32 wx_rs_count_wide(wx_u32 *h, wx_u32 x, int copy
   return KIND == 0 ? (wx_u32)((x & 0x7fffffffu) > 0x7f800000u || x == 0x80000000u) : 0u;
 }
 #define WX_RS_COUNT(x) (wx_sp |= wx_rs_count_wide<KIND, ASC>(h, (x), copy))
-#else
-#define WX_RS_HBLOCK WX_BLOCK
-#define WX_RS_HC WX_RS_HCOPIES
-#define WX_RS_COUNT(x) (wx_sp = 1u, wx_rs_count<KIND, ASC>(h, (x), lane, copy))  // no check: the general map
-#endif
 
 // All four digit histograms in one read: contiguous spans of 16-byte loads
 // (WX_RS_HUNROLL per thread) when the array is 16-byte aligned, scalar
@@ -136,7 +104,6 @@ __device__ __forceinline__ void wx_radix_hist_impl(const WxRadixHistArgs &a) {
     const wx_i64 span = (wx_i64)WX_RS_HBLOCK * WX_RS_HUNROLL;
     const wx_i64 stride = (wx_i64)gridDim.x * span;
     wx_i64 base = (wx_i64)blockIdx.x * span;
-#if WX_RS_HPIPE
     // Whole spans, software-pipelined as wx_project_dense: the next span's
     // loads go out before this span is counted (unconditional loads; guarded
     // ones each wait for the one before and the loop ran latency-bound).
@@ -167,7 +134,6 @@ __device__ __forceinline__ void wx_radix_hist_impl(const WxRadixHistArgs &a) {
         for (int u = 0; u < WX_RS_HUNROLL; ++u) v[u] = w[u];
       }
     }
-#endif
     for (; base < nq; base += stride) {
       u4 v[WX_RS_HUNROLL];
       if (base + span <= nq) {  // workgroup-uniform: unconditional loads, all in flight together
@@ -217,23 +183,9 @@ extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_f_d(WxR
 extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_i_a(WxRadixHistArgs a) { wx_radix_hist_impl<1, true>(a); }
 extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_i_d(WxRadixHistArgs a) { wx_radix_hist_impl<1, false>(a); }
 
-#ifndef WX_RS_SKIP
-// Skip words: a tile still walking back publishes {S: span, sum} for the
-// tiles (p, tile] it has summed (its own count included), so that a
-// successor reading its word jumps the whole span in one read instead of
-// walking the same aggregates again (flag 3; sum in bits 0..39, span - 1 in
-// bits 40..55).  Published when the span reaches WX_RS_SKIP_MIN, then each
-// time it has grown WX_RS_SKIP_GROW-fold.  Measured slower (15.5 vs 13.9 ms
-// per 1e9 keys, profiles/r02/abl_sort_skip.txt): off.
-#define WX_RS_SKIP 0
-#endif
-#ifndef WX_RS_SKIP_MIN
-#define WX_RS_SKIP_MIN 4
-#endif
-#ifndef WX_RS_SKIP_GROW
-#define WX_RS_SKIP_GROW 3
-#endif
-#define WX_RS_SKIP_SUM ((1ull << 40) - 1ull)
+// (Skip words -- a tile still walking back publishing the span it has summed
+// so a successor jumps it in one read -- measured slower, 15.5 vs 13.9 ms per
+// 1e9 keys, profiles/r02/abl_sort_skip.txt; removed in round 5.)
 #ifndef WX_RS_DIAG_LBSTATS
 // diagnostic: digit 0's look-back of every tile counts its rounds, sleeps and
 // the predecessors it walked (ctl words 16 + 8 * pass, a 256-B control
@@ -282,8 +234,6 @@ struct WxRsShared {
   wx_u32 wc[WX_RS_WAVES][256];  // per-wave digit counts, then their exclusive prefix over the waves
   wx_u32 gb[256];  // output slot of digit d's first key minus its tile-local offset
   wx_u32 ld[256];  // tile-local exclusive prefix of the digit counts
-  wx_u32 tt[256];  // the tile's count of digit d (paired look-back)
-  wx_u32 inc[256];  // its wave-inclusive prefix over the digits (paired look-back)
   wx_u32 wsum[4];
   wx_u32 tk[2];  // tile ticket
 };
@@ -539,9 +489,6 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
 #if WX_RS_DIAG_LBSTATS
       wx_u32 lb_rounds = 0, lb_sleeps = 0;
 #endif
-#if WX_RS_SKIP
-      wx_i64 skip_next = WX_RS_SKIP_MIN;  // span at which the next {S} word is published
-#endif
       while (true) {
         wx_u64 wv[WX_RS_LBW];
 #pragma unroll
@@ -552,25 +499,8 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
         fresh = false;
         int stop = WX_RS_LBW;  // index of the first unpublished word
         bool done = false;
-#if WX_RS_SKIP
-        wx_i64 jump = 0;  // a skip word ends the round: the walk resumes at p - jump
-#endif
 #pragma unroll
         for (int j = 0; j < WX_RS_LBW; ++j) {
-#if WX_RS_SKIP
-          if (stop == WX_RS_LBW && !done && jump == 0) {
-            const wx_u64 flag = (wv[j] >> 56) & 3ull;
-            if ((wv[j] >> 58) != (wx_u64)a.epoch || flag == 0ull) {
-              stop = j;
-            } else if (flag == 3ull) {  // {S}: tiles (p - j - span, p - j] summed by a walker
-              excl += wv[j] & WX_RS_SKIP_SUM;
-              jump = j + 1 + (wx_i64)((wv[j] >> 40) & 0xffffull);
-            } else {
-              excl += wv[j] & WX_RS_VAL_MASK;
-              done = flag == 2ull;
-            }
-          }
-#else
           if (stop == WX_RS_LBW && !done) {
             const wx_u64 flag = (wv[j] >> 56) & 3ull;
             if ((wv[j] >> 58) != (wx_u64)a.epoch || flag == 0ull) {
@@ -580,32 +510,16 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
               done = flag == 2ull;
             }
           }
-#endif
         }
 #if WX_RS_DIAG_LBSTATS
         ++lb_rounds;
 #endif
         if (done) break;
-#if WX_RS_SKIP
-        if (jump != 0 || stop == WX_RS_LBW) {
-          p -= jump != 0 ? jump : WX_RS_LBW;
-          t_last = 0ull;  // progress
-          // publish what this walk has summed, own count included, so that
-          // a successor reading this tile's word jumps over the whole span
-          const wx_i64 span = (wx_i64)tile - p;  // tiles (p, tile]
-          if (span >= skip_next && span <= 65536) {
-            wx::st_agent(&row[tid], E | (3ull << 56) | ((wx_u64)(span - 1) << 40) | (excl + tot));
-            skip_next = span * WX_RS_SKIP_GROW;
-          }
-          continue;
-        }
-#else
         if (stop == WX_RS_LBW) {
           p -= WX_RS_LBW;
           t_last = 0ull;  // progress
           continue;
         }
-#endif
         if (stop > 0) t_last = 0ull;
         p -= stop;
 #if WX_RS_DIAG_LBSTATS
@@ -643,139 +557,10 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
   }
 }
 
-#ifndef WX_RS_LB_PAIR
-// Paired look-back (key tiles): digit d's walk is shared by lanes 2d and
-// 2d + 1 of the whole 512-thread tile (waves 4-7 used to idle through it),
-// each loading WX_RS_LBW predecessor words per round -- half 0 the nearer,
-// half 1 the next ones -- and combining their partial results with one
-// lane shuffle, so a round covers 2 x WX_RS_LBW predecessors at the
-// registers of WX_RS_LBW (128 VGPRs, no spill).  Correct, and slower: 14.60
-// vs 13.72 ms per 1e9 float keys in one process, three alternating rounds
-// (profiles/r03/abl_sort_lbpair.txt) -- the walk waits on predecessors that
-// have not published yet far more than it walks published ones, and the
-// doubled poll traffic costs more than the halved round count saves.  Off.
-#define WX_RS_LB_PAIR 0
-#endif
-// As wx_rs_digits, with the look-back of digit tid >> 1 on lane pair
-// (tid & ~1, tid | 1): every thread of the tile holds this function's barrier.
-__device__ __forceinline__ void wx_rs_digits_pair(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const wx_u64 E = (wx_u64)a.epoch << 58;
-  const bool look = tile != 0 && !WX_RS_DIAG_NO_LOOKBACK;
-  if (tid < 256) {
-    wx_u32 tot = 0u;
-#pragma unroll
-    for (int w = 0; w < WX_RS_WAVES; ++w) {
-      const wx_u32 c = S.wc[w][tid];
-      S.wc[w][tid] = tot;
-      tot += c;
-    }
-    wx::st_agent(&a.status[(wx_u64)tile * 256 + tid], E | (look ? WX_RS_FLAG_A : WX_RS_FLAG_P) | tot);
-    wx_u32 inc = tot;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const wx_u32 t = __shfl_up(inc, o);
-      if (lane >= o) inc += t;
-    }
-    if (lane == 63) S.wsum[wave] = inc;
-    S.tt[tid] = tot;
-    S.inc[tid] = inc;
-  }
-  const int d = tid >> 1, h = tid & 1;
-  // this half's first round, in flight across the barrier
-  wx_i64 p = (wx_i64)tile - 1;
-  wx_u64 wv[WX_RS_LBW];
-#pragma unroll
-  for (int j = 0; j < WX_RS_LBW; ++j) {
-    const wx_i64 q = p - h * WX_RS_LBW - j;
-    wv[j] = (look && q >= 0) ? wx::ld_agent(&a.status[(wx_u64)q * 256 + d]) : (E | WX_RS_FLAG_P);
-  }
-  __syncthreads();
-  wx_u64 excl = 0;
-  if (look) {
-    wx_u32 spins = 0;
-    wx_u64 t_last = 0ull;
-    bool fresh = true;
-    while (true) {
-      if (!fresh) {
-#pragma unroll
-        for (int j = 0; j < WX_RS_LBW; ++j) {
-          const wx_i64 q = p - h * WX_RS_LBW - j;
-          wv[j] = q >= 0 ? wx::ld_agent(&a.status[(wx_u64)q * 256 + d]) : (E | WX_RS_FLAG_P);
-        }
-      }
-      fresh = false;
-      // this half: index of its first unpublished word, whether a {P} comes
-      // before it, the sum up to either
-      int stop = WX_RS_LBW;
-      bool done = false;
-      wx_u64 sum = 0;
-#pragma unroll
-      for (int j = 0; j < WX_RS_LBW; ++j) {
-        if (stop == WX_RS_LBW && !done) {
-          const wx_u64 flag = (wv[j] >> 56) & 3ull;
-          if ((wv[j] >> 58) != (wx_u64)a.epoch || flag == 0ull) {
-            stop = j;
-          } else {
-            sum += wv[j] & WX_RS_VAL_MASK;
-            done = flag == 2ull;
-          }
-        }
-      }
-      const int o_stop = __shfl_xor(stop, 1);
-      const int o_done = __shfl_xor((int)done, 1);
-      const wx_u64 o_sum = __shfl_xor(sum, 1);
-      // near = half 0's words, far = half 1's
-      const int n_stop = h ? o_stop : stop, f_stop = h ? stop : o_stop;
-      const bool n_done = h ? o_done != 0 : done, f_done = h ? done : o_done != 0;
-      const wx_u64 n_sum = h ? o_sum : sum, f_sum = h ? sum : o_sum;
-      excl += n_sum;
-      int adv;  // predecessors consumed this round
-      bool fin = false;
-      if (n_stop < WX_RS_LBW) {
-        adv = n_stop;
-      } else if (n_done) {
-        fin = true;
-        adv = 0;
-      } else {
-        excl += f_sum;
-        if (f_stop < WX_RS_LBW) adv = WX_RS_LBW + f_stop;
-        else if (f_done) { fin = true; adv = 0; }
-        else adv = 2 * WX_RS_LBW;
-      }
-      if (fin) break;
-      p -= adv;
-      if (adv == 2 * WX_RS_LBW) {
-        t_last = 0ull;  // progress
-        continue;
-      }
-      if (adv > 0) t_last = 0ull;
-      __builtin_amdgcn_s_sleep(1);
-      if ((++spins & 63u) == 0u) {
-        const wx_u64 now = __builtin_amdgcn_s_memrealtime();
-        if (t_last == 0ull) {
-          t_last = now;
-        } else if (now - t_last > WX_STALL_TICKS) {
-          atomicOr(a.err, WX_DEVERR_LOOKBACK);
-          atomicExch(&a.ctl[1], 1u);
-        }
-        if (__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-      }
-    }
-  }
-  if (h == 0) {
-    const wx_u32 tot = S.tt[d];
-    wx_u32 ld = S.inc[d] - tot;
-    for (int w = 0; w < (d >> 6); ++w) ld += S.wsum[w];
-    if (WX_RS_FOLD_LD) {
-#pragma unroll
-      for (int w = 0; w < WX_RS_WAVES; ++w) S.wc[w][d] += ld;
-    }
-    if (look) wx::st_agent(&a.status[(wx_u64)tile * 256 + d], E | WX_RS_FLAG_P | (excl + tot));
-    S.gb[d] = a.digit_base[d] + (wx_u32)excl - ld;
-    S.ld[d] = ld;
-  }
-}
+// (A paired look-back -- digit d's walk shared by lanes 2d and 2d + 1, a
+// round covering 2 x WX_RS_LBW predecessors -- was correct and slower,
+// 14.60 vs 13.72 ms per 1e9 float keys, profiles/r03/abl_sort_lbpair.txt;
+// removed in round 5.)
 
 #ifndef WX_RS_SPLIT
 // 1: the keys (and payloads) are permuted into LDS by their tile-local
@@ -1032,10 +817,7 @@ __device__ __forceinline__ void wx_radix_tile_body(const WxRadixPassArgs &a, WxR
     wx_rs_scatter<KIND, ASC, WHOLE>(a, S, wb, x, rk, pos, s_k);
     if (tid < 256) wx_rs_resolve(a, S, tile, tot, first);
   } else {
-    if (WX_RS_LB_PAIR && !PAY && WX_RS_BLOCK == 512)
-      wx_rs_digits_pair(a, S, tile);
-    else
-      wx_rs_digits(a, S, tile);
+    wx_rs_digits(a, S, tile);
     __syncthreads();
     WX_RS_STAMP(4);
     wx_rs_scatter<KIND, ASC, WHOLE>(a, S, wb, x, rk, pos, s_k);

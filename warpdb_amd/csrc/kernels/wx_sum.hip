@@ -8,7 +8,7 @@
 // WX_UNROLL row quads in flight per thread; one partial per block, combined
 // in a fixed order by wx_sum_finalize (bitwise reproducible).
 #ifndef WX_UNROLL
-#define WX_UNROLL 8  // tools/ablate_stream.py: 8 quads in flight, 8 workgroups per CU
+#define WX_UNROLL 8  // profiles/r01/ablate_stream.txt: 8 quads in flight, 8 workgroups per CU
 #endif
 #ifndef WX_MINMAX
 #define WX_MINMAX 0  // also MIN / MAX of the passing values (NaN skipped)
