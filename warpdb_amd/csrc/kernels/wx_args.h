@@ -45,7 +45,7 @@ typedef unsigned int wx_u32;
 // one tile = WX_RS_BLOCK threads x WX_RS_ITEMS keys, one 64-bit look-back
 // status word per (tile, digit).
 #ifndef WX_RS_BLOCK
-#define WX_RS_BLOCK 512  // >= 256: threads 0..255 own one digit each
+#define WX_RS_BLOCK 1024  // >= 256: threads 0..255 own one digit each
 #endif
 #ifndef WX_RS_ITEMS
 #define WX_RS_ITEMS 32
