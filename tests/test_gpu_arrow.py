@@ -83,13 +83,12 @@ def write_csv(path, cols):
 
 
 @pytest.fixture(scope="module")
-def big_db():
+def big_db(tmp_path_factory):
     from warpdb_amd import pywarpdb as pw
 
     n = 2_000_003
     cols = synth.c2_table(n)
-    path = os.path.join(ROOT, "gpurun_out", "arrow_big.csv")
-    os.makedirs(os.path.dirname(path), exist_ok=True)
+    path = str(tmp_path_factory.mktemp("arrow") / "arrow_big.csv")
     write_csv(path, cols)
     return pw.WarpDB(path), cols
 

@@ -121,7 +121,7 @@ struct WxRoShared {
 // unconditionally), then bound like the streamed registers
 #define WX_RO_DECL(name, T, slot) T wx_n##slot[WX_RO_ITEMS];
 #define WX_RO_LOAD(name, T, slot) \
-  wx_n##slot[i] = (WHOLE || e < wx_a.n_rows) ? static_cast<const T *>(wx_a.col[slot])[e] : T(0);
+  wx_n##slot[i] = (WHOLE || e < wx_a.n_rows) ? static_cast<const T *>(wx_a.col[slot])[e] : static_cast<T>(0);
 #define WX_RO_BIND(name, T, slot) const ::wx::reg<T> name{wx_n##slot[i]};
 
 // Tile t of range r (run[]: the range's next output slot of this thread's

@@ -70,8 +70,6 @@ struct WxTableView {
 
 // Host <-> HBM copies (transfer.cpp).  copy_h2d may return before the DMA
 // finishes (the source is already staged); copy_d2h returns with `dst` filled.
-enum class TransferMode { Pageable, Staged, Register };
-TransferMode transfer_mode();  // $WARPDB_H2D: pageable (default) | staged | register
 void copy_h2d(int device, hipStream_t s, void *dst, const void *src, size_t bytes);
 void copy_d2h(int device, hipStream_t s, void *dst, const void *src, size_t bytes);
 // A zero-filled host result of n floats (huge-page backed when large).

@@ -18,7 +18,6 @@
 #include <condition_variable>
 #include <cstring>
 #include <exception>
-#include <future>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -915,29 +914,11 @@ std::vector<float> run_multi_gpu_jit_host(const HostTable &host, const std::stri
   using namespace warpdb;
   const int64_t n = host.num_rows();
   auto shards = plan_shards(n, shard_count());
-  // The host result (4 B/row, first-touch bound) is allocated on its own
-  // thread while the devices upload and compute; downloads wait for it.
-  std::vector<float> result;
-  std::promise<void> ready;
-  std::shared_future<void> result_ready = ready.get_future().share();
-  auto make_result = [&] {
-    try {
-      result = host_result(static_cast<size_t>(n));
-      ready.set_value();
-    } catch (...) {
-      ready.set_exception(std::current_exception());
-    }
-  };
-  const bool serial_alloc = std::string(std::getenv("WARPDB_HOST_ALLOC") ? std::getenv("WARPDB_HOST_ALLOC") : "serial") ==
-                            "serial";
-  if (serial_alloc) make_result();
-  std::thread alloc([&] {
-    if (!serial_alloc) make_result();
-  });
-  struct Join {
-    std::thread &t;
-    ~Join() { t.join(); }
-  } join{alloc};
+  // The host result (4 B/row, first-touch bound) is allocated and populated
+  // before the uploads: populating it on a thread of its own while the
+  // runtime stages the pageable uploads slowed both, 31 vs 27-29 ms per 1e8
+  // rows (profiles/r01/host_pipeline_alloc_mode.txt).
+  std::vector<float> result = host_result(static_cast<size_t>(n));
   // Per device, a chunked pipeline over its shard: this thread uploads chunk
   // c and runs the dense kernel on it (stream 0) while a second thread
   // downloads chunk c - 1 (stream 1), so the two PCIe directions overlap
@@ -1004,8 +985,6 @@ std::vector<float> run_multi_gpu_jit_host(const HostTable &host, const std::stri
     std::thread down([&] {
       try {
         DevGuard g(r.device);
-        result_ready.get();
-        stamp("result ready", r.device, -1);
         for (int64_t c = 0; c < n_chunks; ++c) {
           {
             std::unique_lock<std::mutex> lk(mu);
@@ -1068,6 +1047,5 @@ std::vector<float> run_multi_gpu_jit_host(const HostTable &host, const std::stri
     if (d2h_err) std::rethrow_exception(d2h_err);
     hip_ok(hipStreamSynchronize(s2), "hipStreamSynchronize");
   });
-  result_ready.get();  // n == 0: no device ran
   return result;
 }
