@@ -809,25 +809,30 @@ def test_concurrent_streams_from_threads():
 
     def work(j):
         table, price, _, want, b, stream = jobs[j]
+        op, it = "setup", -1
         try:
             with torch.cuda.stream(stream):
                 L = wx.make_launch(device=0, stream=stream.cuda_stream, custom_src=DISCOUNT_SRC, flags=wx.F_SYNC)
                 for it in range(iters):
+                    op = "compact"
                     cnt = wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", L,
                                             wx.MODE_COMPACT, b["vals"].data_ptr(), b["idx"].data_ptr(), 8, 0,
                                             want_count=True)
                     assert cnt == want["idx"].numel()
                     assert torch.equal(b["idx"][:cnt], want["idx"]) and torch.equal(b["vals"][:cnt], want["vals"])
+                    op = "sum"
                     assert wx.reduce_sum(table, "(price[idx] * 0.9f)", "(price[idx] > 20.0f)", L) == want["sum"]
+                    op = "topk"
                     wx.topk(table, "price[idx]", None, "discount(price[idx], 0.9f)", 5, True, L, b["k"].data_ptr(),
                             b["i"].data_ptr(), b["v"].data_ptr())
                     assert all(torch.equal(x, y) for x, y in zip((b["k"], b["i"], b["v"]), want["topk"]))
+                    op = "sort"
                     b["sort"].copy_(price)
                     wx.sort_float(b["sort"].data_ptr(), table.n_rows, True, L)
                     assert torch.equal(b["sort"], want["sorted"]), it
                 stream.synchronize()
         except Exception as e:  # noqa: BLE001 - reported by the main thread
-            errors.append((j, repr(e)))
+            errors.append((j, op, it, repr(e)))
 
     th = [threading.Thread(target=work, args=(j,)) for j in range(n_threads)]
     for t in th:

@@ -43,6 +43,10 @@ __device__ __forceinline__ wx_u64 wx_cflag(wx_u64 w, wx_u64 E) {
 // another process sharing the GPU still completes.
 #define WX_STALL_TICKS 200000000ull  // 2 s
 #endif
+// ... and only after this many polls without progress as well: a wave that
+// is descheduled (the queue preempted) polls nothing, so a long preemption
+// alone never reads as a stall (>= 65 ms of polling at >= 1 us per poll)
+#define WX_STALL_SPINS (1u << 16)
 #ifndef WX_LB_PER_LANE
 #define WX_LB_PER_LANE 1  // predecessors per lane per look-back round (1 measured fastest: each agent-scope poll is costly)
 #endif
@@ -109,7 +113,8 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
         if (__builtin_amdgcn_ballot_w64(moved) != 0ull || t_last == 0ull) {
           t_last = now;
           moved = false;
-        } else if (now - t_last > WX_STALL_TICKS) {  // sticky error for the host + this launch's abort word
+          spins = 0;
+        } else if (now - t_last > WX_STALL_TICKS && spins >= WX_STALL_SPINS) {  // sticky error for the host + this launch's abort word
           atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_LOOKBACK);
           wx::st_agent(&a.status[a.n_tiles], abort_word);
         }
@@ -127,6 +132,7 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
     if (near_p < 64 * WX_LB_PER_LANE) break;
     look -= 64 * WX_LB_PER_LANE;
     t_last = 0ull;  // the window moved: progress
+    spins = 0;
   }
   return excl;
 }

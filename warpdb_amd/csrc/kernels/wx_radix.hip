@@ -40,6 +40,7 @@
 #ifndef WX_STALL_TICKS
 #define WX_STALL_TICKS 200000000ull  // 2 s at 100 MHz without progress (see the compaction look-back)
 #endif
+#define WX_STALL_SPINS (1u << 16)  // and this many polls: a descheduled wave polls nothing
 #define WX_RS_FLAG_A (1ull << 56)
 #define WX_RS_FLAG_P (2ull << 56)
 #define WX_RS_VAL_MASK ((1ull << 56) - 1ull)
@@ -518,9 +519,10 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
         if (stop == WX_RS_LBW) {
           p -= WX_RS_LBW;
           t_last = 0ull;  // progress
+          spins = 0;
           continue;
         }
-        if (stop > 0) t_last = 0ull;
+        if (stop > 0) t_last = 0ull, spins = 0;
         p -= stop;
 #if WX_RS_DIAG_LBSTATS
         ++lb_sleeps;
@@ -531,7 +533,7 @@ __device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShare
           const wx_u64 now = __builtin_amdgcn_s_memrealtime();
           if (t_last == 0ull) {
             t_last = now;
-          } else if (now - t_last > WX_STALL_TICKS) {
+          } else if (now - t_last > WX_STALL_TICKS && spins >= WX_STALL_SPINS) {
             atomicOr(a.err, WX_DEVERR_LOOKBACK);
             atomicExch(&a.ctl[1], 1u);
           }
@@ -649,16 +651,17 @@ __device__ __forceinline__ void wx_rs_resolve(const WxRadixPassArgs &a, WxRsShar
       if (stop == WX_RS_LBW) {
         p -= WX_RS_LBW;
         t_last = 0ull;
+        spins = 0;
         continue;
       }
-      if (stop > 0) t_last = 0ull;
+      if (stop > 0) t_last = 0ull, spins = 0;
       p -= stop;
       __builtin_amdgcn_s_sleep(1);
       if ((++spins & 63u) == 0u) {
         const wx_u64 now = __builtin_amdgcn_s_memrealtime();
         if (t_last == 0ull) {
           t_last = now;
-        } else if (now - t_last > WX_STALL_TICKS) {
+        } else if (now - t_last > WX_STALL_TICKS && spins >= WX_STALL_SPINS) {
           atomicOr(a.err, WX_DEVERR_LOOKBACK);
           atomicExch(&a.ctl[1], 1u);
         }
