@@ -199,14 +199,8 @@ extern "C" __global__ __launch_bounds__(WX_RS_HBLOCK) void wx_radix_hist_i_d(WxR
 #ifndef WX_RS_RANK_LEAD
 #define WX_RS_RANK_LEAD 1  // lane 0's digit group ranked by one ballot, without LDS
 #endif
-#ifndef WX_RS_LB_FIRST
-#define WX_RS_LB_FIRST 1  // load the first predecessor word before the in-tile scan's barrier (13.61-13.75 vs 13.83 ms, abl_sort_lbfirst.txt)
-#endif
 #ifndef WX_RS_DIAG_NO_RANK
 #define WX_RS_DIAG_NO_RANK 0  // diagnostic: no in-wave ranking, keys keep their slots (results invalid)
-#endif
-#ifndef WX_RS_NT_STORE
-#define WX_RS_NT_STORE 1  // nontemporal stores: keys 14.27 -> 14.01 ms per 1e9 (abl_sort_nt.txt); the pair module sets 0
 #endif
 #ifndef WX_RS_DIAG_NO_STORE
 #define WX_RS_DIAG_NO_STORE 0  // diagnostic: keys are read out of LDS but not written (results invalid)
@@ -258,13 +252,10 @@ __device__ __forceinline__ void wx_rs_load(const WxRadixPassArgs &a, wx_i64 wb, 
   }
 }
 
-#ifndef WX_RS_FOLD_LD
-// the digit's tile-local base folded into the per-wave counts once per tile
-// (2 048 adds), so the permutation reads one LDS word per key, not two:
+// The digit's tile-local base is folded into the per-wave counts once per
+// tile (2 048 adds), so the permutation reads one LDS word per key, not two:
 // 12.6 vs 12.8 ms per 1e9 float keys with the atomic ranking, 13.45 vs 13.75
-// without (abl_sort_fold.txt)
-#define WX_RS_FOLD_LD 1
-#endif
+// without (abl_sort_fold.txt).
 #ifndef WX_RS_RANK_ATOMIC
 // Rank by one returning LDS add per key (ds_add_rtn_u32 on the wave's digit
 // counter): the LDS serialises the lanes of one instruction that hit the
@@ -441,138 +432,111 @@ __device__ __forceinline__ void wx_rs_rank(const WxRadixPassArgs &a, WxRsShared 
   }
 }
 
-// Threads 0..255, digit d = tid: publish the tile's count of digit d ({A},
-// or {P} for tile 0) as soon as the per-wave counts are summed, then the
-// exclusive prefix over the waves and over the digits, look back to an
-// inclusive {P}, publish it; fills S.gb / S.ld.  Called by every thread (it
-// holds a barrier).  Publishing before the in-tile scan and its barrier
-// rather than after: 17.0 vs 17.5 ms per 1e9 keys (ablate_sort.txt).
-__device__ __forceinline__ void wx_rs_digits(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile) {
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// (Round 5: the walk spread over 2 or 4 lanes per digit -- lane q loading
+// the q-th group of WX_RS_LBW words, the parts combined in order by DPP
+// broadcasts -- was correct and slower, 11.77 vs 11.23 ms per 1e9 float keys
+// at 1024 x 32 and 19.14 vs 18.58 per 1e9 pairs, profiles/r05/
+// ab_sort_lb_lanes.txt: one lane per digit walks.)
+
+// Exclusive prefix of digit d over the tiles before `tile`: a walk back
+// from tile - 1 summing {A} / {P} words to the first {P}, WX_RS_LBW words
+// per round (`first`: the first round, loaded earlier).
+__device__ __forceinline__ wx_u64 wx_rs_walk(const WxRadixPassArgs &a, wx_u32 tile, int d,
+                                             const wx_u64 (&first)[WX_RS_LBW]) {
   const wx_u64 E = (wx_u64)a.epoch << 58;
-  wx_u64 *row = a.status + (wx_u64)tile * 256;
-  const bool look = tile != 0 && !WX_RS_DIAG_NO_LOOKBACK;
-  wx_u32 tot = 0u, inc = 0u;
-  wx_u64 first = 0ull;  // the first predecessor word, loaded before the barrier
-  if (tid < 256) {
+  wx_i64 p = (wx_i64)tile - 1;  // the nearest predecessor not yet summed
+  wx_u64 excl = 0;
+  wx_u32 spins = 0;
+  wx_u64 t_last = 0ull;  // time of the last progress (0: not yet sampled)
+  bool fresh = true;
+#if WX_RS_DIAG_LBSTATS
+  wx_u32 lb_rounds = 0, lb_sleeps = 0;
+#endif
+  while (true) {
+    wx_u64 wv[WX_RS_LBW];
 #pragma unroll
-    for (int w = 0; w < WX_RS_WAVES; ++w) {
-      const wx_u32 c = S.wc[w][tid];
-      S.wc[w][tid] = tot;
-      tot += c;
-    }
-    wx::st_agent(&row[tid], E | (look ? WX_RS_FLAG_A : WX_RS_FLAG_P) | tot);
-    if (WX_RS_LB_FIRST && look) first = wx::ld_agent(&a.status[(wx_u64)(tile - 1) * 256 + tid]);
-    inc = tot;
+    for (int j = 0; j < WX_RS_LBW; ++j)
+      wv[j] = fresh ? first[j] : p - j >= 0 ? wx::ld_agent(&a.status[(wx_u64)(p - j) * 256 + d]) : (E | WX_RS_FLAG_P);
+    fresh = false;
+    int stop = WX_RS_LBW;  // index of the first unpublished word
+    bool done = false;
 #pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const wx_u32 t = __shfl_up(inc, o);
-      if (lane >= o) inc += t;
+    for (int j = 0; j < WX_RS_LBW; ++j) {
+      if (stop == WX_RS_LBW && !done) {
+        const wx_u64 flag = (wv[j] >> 56) & 3ull;
+        if ((wv[j] >> 58) != (wx_u64)a.epoch || flag == 0ull) {
+          stop = j;
+        } else {
+          excl += wv[j] & WX_RS_VAL_MASK;
+          done = flag == 2ull;
+        }
+      }
     }
-    if (lane == 63) S.wsum[wave] = inc;
+#if WX_RS_DIAG_LBSTATS
+    ++lb_rounds;
+#endif
+    if (done) break;
+    if (stop == WX_RS_LBW) {
+      p -= WX_RS_LBW;
+      t_last = 0ull;  // progress
+      spins = 0;
+      continue;
+    }
+    if (stop > 0) t_last = 0ull, spins = 0;
+    p -= stop;
+#if WX_RS_DIAG_LBSTATS
+    ++lb_sleeps;
+#endif
+    if (WX_RS_SLEEP) __builtin_amdgcn_s_sleep(WX_RS_SLEEP);
+    if ((++spins & 63u) == 0u) {
+      // abort only after WX_STALL_TICKS and WX_STALL_SPINS with this digit's chain not moving
+      const wx_u64 now = __builtin_amdgcn_s_memrealtime();
+      if (t_last == 0ull) {
+        t_last = now;
+      } else if (now - t_last > WX_STALL_TICKS && spins >= WX_STALL_SPINS) {
+        atomicOr(a.err, WX_DEVERR_LOOKBACK);
+        atomicExch(&a.ctl[1], 1u);
+      }
+      if (__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
+    }
   }
-  __syncthreads();
-  if (tid < 256) {
-    wx_u32 ld = inc - tot;
-    for (int w = 0; w < wave; ++w) ld += S.wsum[w];
-    if (WX_RS_FOLD_LD) {
+#if WX_RS_DIAG_LBSTATS
+  if (threadIdx.x == 0) {
+    wx_u32 *st = a.ctl + 16 + 6 * (a.shift / 8);  // = control word 16 + 8 * pass
+    atomicAdd(&st[0], lb_rounds);
+    atomicAdd(&st[1], lb_sleeps);
+    atomicAdd(&st[2], (wx_u32)((wx_i64)tile - 1 - p));
+    __threadfence();
+    if (atomicAdd(&st[3], 1u) == (wx_u32)((a.n + WX_RS_TILE - 1) / WX_RS_TILE) - 2u)
+      printf("[lbstats] pass %d tiles %u rounds %u sleeps %u walked %u\n", a.shift / 8, atomicAdd(&st[3], 0u) + 1u,
+             atomicAdd(&st[0], 0u), atomicAdd(&st[1], 0u), atomicAdd(&st[2], 0u));
+  }
+#endif
+  return excl;
+}
+
+// The first round of digit d's walk, issued early so the loads fly across
+// a barrier.
+__device__ __forceinline__ void wx_rs_walk_first(const WxRadixPassArgs &a, wx_u32 tile, int d,
+                                                 wx_u64 (&first)[WX_RS_LBW]) {
+  const wx_u64 E = (wx_u64)a.epoch << 58;
 #pragma unroll
-      for (int w = 0; w < WX_RS_WAVES; ++w) S.wc[w][tid] += ld;  // the scatter's slot base in one word
-    }
-    wx_u64 excl = 0;
-    if (look) {
-      // WX_RS_LBW predecessors per round, loads in flight together; stop at
-      // the first unpublished word (re-polled from there) or the first {P}
-      wx_i64 p = (wx_i64)tile - 1;
-      wx_u32 spins = 0;
-      wx_u64 t_last = 0ull;  // time of the last progress (0: not yet sampled)
-      bool fresh = WX_RS_LB_FIRST;
-#if WX_RS_DIAG_LBSTATS
-      wx_u32 lb_rounds = 0, lb_sleeps = 0;
-#endif
-      while (true) {
-        wx_u64 wv[WX_RS_LBW];
-#pragma unroll
-        for (int j = 0; j < WX_RS_LBW; ++j)
-          wv[j] = (j == 0 && fresh) ? first
-                  : p - j >= 0    ? wx::ld_agent(&a.status[(wx_u64)(p - j) * 256 + tid])
-                                  : (E | WX_RS_FLAG_P);
-        fresh = false;
-        int stop = WX_RS_LBW;  // index of the first unpublished word
-        bool done = false;
-#pragma unroll
-        for (int j = 0; j < WX_RS_LBW; ++j) {
-          if (stop == WX_RS_LBW && !done) {
-            const wx_u64 flag = (wv[j] >> 56) & 3ull;
-            if ((wv[j] >> 58) != (wx_u64)a.epoch || flag == 0ull) {
-              stop = j;
-            } else {
-              excl += wv[j] & WX_RS_VAL_MASK;
-              done = flag == 2ull;
-            }
-          }
-        }
-#if WX_RS_DIAG_LBSTATS
-        ++lb_rounds;
-#endif
-        if (done) break;
-        if (stop == WX_RS_LBW) {
-          p -= WX_RS_LBW;
-          t_last = 0ull;  // progress
-          spins = 0;
-          continue;
-        }
-        if (stop > 0) t_last = 0ull, spins = 0;
-        p -= stop;
-#if WX_RS_DIAG_LBSTATS
-        ++lb_sleeps;
-#endif
-        if (WX_RS_SLEEP) __builtin_amdgcn_s_sleep(WX_RS_SLEEP);
-        if ((++spins & 63u) == 0u) {
-          // abort only after WX_STALL_TICKS with this digit's chain not moving
-          const wx_u64 now = __builtin_amdgcn_s_memrealtime();
-          if (t_last == 0ull) {
-            t_last = now;
-          } else if (now - t_last > WX_STALL_TICKS && spins >= WX_STALL_SPINS) {
-            atomicOr(a.err, WX_DEVERR_LOOKBACK);
-            atomicExch(&a.ctl[1], 1u);
-          }
-          if (__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-        }
-      }
-      wx::st_agent(&row[tid], E | WX_RS_FLAG_P | (excl + tot));
-#if WX_RS_DIAG_LBSTATS
-      if (tid == 0) {
-        wx_u32 *st = a.ctl + 16 + 6 * (a.shift / 8);  // = control word 16 + 8 * pass
-        atomicAdd(&st[0], lb_rounds);
-        atomicAdd(&st[1], lb_sleeps);
-        atomicAdd(&st[2], (wx_u32)((wx_i64)tile - 1 - p));
-        __threadfence();
-        if (atomicAdd(&st[3], 1u) == (wx_u32)((a.n + WX_RS_TILE - 1) / WX_RS_TILE) - 2u)
-          printf("[lbstats] pass %d tiles %u rounds %u sleeps %u walked %u\n", a.shift / 8, atomicAdd(&st[3], 0u) + 1u,
-                 atomicAdd(&st[0], 0u), atomicAdd(&st[1], 0u), atomicAdd(&st[2], 0u));
-      }
-#endif
-    }
-    S.gb[tid] = a.digit_base[tid] + (wx_u32)excl - ld;
-    S.ld[tid] = ld;
+  for (int j = 0; j < WX_RS_LBW; ++j) {
+    const wx_i64 t = (wx_i64)tile - 1 - j;
+    first[j] = t >= 0 ? wx::ld_agent(&a.status[(wx_u64)t * 256 + d]) : (E | WX_RS_FLAG_P);
   }
 }
 
-// (A paired look-back -- digit d's walk shared by lanes 2d and 2d + 1, a
-// round covering 2 x WX_RS_LBW predecessors -- was correct and slower,
-// 14.60 vs 13.72 ms per 1e9 float keys, profiles/r03/abl_sort_lbpair.txt;
-// removed in round 5.)
-
-#ifndef WX_RS_SPLIT
-// 1: the keys (and payloads) are permuted into LDS by their tile-local
-// slots, which need only this tile's counts, before the look-back resolves
-// the tile's global offsets: the permutation overlaps the look-back's first
-// poll instead of waiting behind the whole look-back.  Key + payload tiles:
-// 19.8 vs 21.8 ms per 1e9 pairs; keys alone lose the extra barrier's worth
-// (15.4 vs 14.9 ms), so only the pair module sets it (abl_sort_split.txt).
-#define WX_RS_SPLIT 0
-#endif
+// The keys (and payloads) are permuted into LDS by their tile-local slots,
+// which need only this tile's counts, before the look-back resolves the
+// tile's global offsets: the permutation overlaps the look-back's first
+// poll instead of waiting behind the whole look-back.  Key + payload tiles
+// since round 2 (19.8 vs 21.8 ms per 1e9 pairs); keys since round 5, with the
+// 1024 x 32 tile and plain stores: 8.67 ms per 1e9 float keys against 9.30
+// with nontemporal stores, 9.81 unsplit and 10.08 unsplit with nontemporal
+// stores (round 4's form), one process (profiles/r05/ab_sort_split_store.txt;
+// round 2 at 512 x 32 had measured the split slower for keys, 15.4 vs 14.9).
+// The unsplit form and the nontemporal stores were removed in round 5.
 // Split form, part 1 (every thread; holds a barrier): threads 0..255 own
 // digit tid, publish its count {A} (or {P} for tile 0), then the exclusive
 // prefix over the waves (S.wc) and over the digits (S.ld).  Returns the
@@ -603,73 +567,21 @@ __device__ __forceinline__ wx_u32 wx_rs_local(const WxRadixPassArgs &a, WxRsShar
     wx_u32 ld = inc - tot;
     for (int w = 0; w < wave; ++w) ld += S.wsum[w];
     S.ld[tid] = ld;
-    if (WX_RS_FOLD_LD) {
 #pragma unroll
-      for (int w = 0; w < WX_RS_WAVES; ++w) S.wc[w][tid] += ld;
-    }
+    for (int w = 0; w < WX_RS_WAVES; ++w) S.wc[w][tid] += ld;
   }
   return tot;
 }
 
-// Split form, part 2 (threads 0..255): look back over the preceding tiles'
-// words of digit tid to an inclusive {P} (`first` is predecessor tile - 1's
-// word, loaded earlier), publish {P}, set S.gb.
+// Split form, part 2 (threads 0..255): walk back for digit tid (`first`:
+// the walk's first round, loaded earlier), publish {P}, set S.gb.
 __device__ __forceinline__ void wx_rs_resolve(const WxRadixPassArgs &a, WxRsShared &S, wx_u32 tile, wx_u32 tot,
-                                              wx_u64 first) {
+                                              const wx_u64 (&first)[WX_RS_LBW]) {
   const int tid = threadIdx.x;
   const wx_u64 E = (wx_u64)a.epoch << 58;
   const bool look = tile != 0 && !WX_RS_DIAG_NO_LOOKBACK;
-  wx_u64 excl = 0;
-  if (look) {
-    wx_i64 p = (wx_i64)tile - 1;
-    wx_u32 spins = 0;
-    wx_u64 t_last = 0ull;
-    bool fresh = true;
-    while (true) {
-      wx_u64 wv[WX_RS_LBW];
-#pragma unroll
-      for (int j = 0; j < WX_RS_LBW; ++j)
-        wv[j] = (j == 0 && fresh) ? first
-                : p - j >= 0    ? wx::ld_agent(&a.status[(wx_u64)(p - j) * 256 + tid])
-                                : (E | WX_RS_FLAG_P);
-      fresh = false;
-      int stop = WX_RS_LBW;
-      bool done = false;
-#pragma unroll
-      for (int j = 0; j < WX_RS_LBW; ++j) {
-        if (stop == WX_RS_LBW && !done) {
-          const wx_u64 flag = (wv[j] >> 56) & 3ull;
-          if ((wv[j] >> 58) != (wx_u64)a.epoch || flag == 0ull) {
-            stop = j;
-          } else {
-            excl += wv[j] & WX_RS_VAL_MASK;
-            done = flag == 2ull;
-          }
-        }
-      }
-      if (done) break;
-      if (stop == WX_RS_LBW) {
-        p -= WX_RS_LBW;
-        t_last = 0ull;
-        spins = 0;
-        continue;
-      }
-      if (stop > 0) t_last = 0ull, spins = 0;
-      p -= stop;
-      __builtin_amdgcn_s_sleep(1);
-      if ((++spins & 63u) == 0u) {
-        const wx_u64 now = __builtin_amdgcn_s_memrealtime();
-        if (t_last == 0ull) {
-          t_last = now;
-        } else if (now - t_last > WX_STALL_TICKS && spins >= WX_STALL_SPINS) {
-          atomicOr(a.err, WX_DEVERR_LOOKBACK);
-          atomicExch(&a.ctl[1], 1u);
-        }
-        if (__hip_atomic_load(&a.ctl[1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) break;
-      }
-    }
-    wx::st_agent(&a.status[(wx_u64)tile * 256 + tid], E | WX_RS_FLAG_P | (excl + tot));
-  }
+  const wx_u64 excl = look ? wx_rs_walk(a, tile, tid, first) : 0ull;
+  if (look) wx::st_agent(&a.status[(wx_u64)tile * 256 + tid], E | WX_RS_FLAG_P | (excl + tot));
   S.gb[tid] = a.digit_base[tid] + (wx_u32)excl - S.ld[tid];
 }
 
@@ -685,7 +597,7 @@ __device__ __forceinline__ void wx_rs_scatter(const WxRadixPassArgs &a, WxRsShar
     wx_u32 p = 0u;
     if (WHOLE || wb + (wx_i64)i * 64 < a.n) {
       const wx_u32 d = (wx_rs_key_t<KIND, ASC>(x[i]) >> a.shift) & 255u;
-      p = (WX_RS_FOLD_LD ? 0u : S.ld[d]) + S.wc[wave][d] + rk[i];
+      p = S.wc[wave][d] + rk[i];
       if (WX_RS_DIAG_NO_RANK) p = (wx_u32)(wave * 64 * WX_RS_ITEMS + i * 64 + (threadIdx.x & 63));
       s_k[p] = x[i];
     }
@@ -709,10 +621,8 @@ __device__ __forceinline__ void wx_rs_store(const WxRadixPassArgs &a, const WxRs
       if (WX_RS_DIAG_NO_LOOKBACK || WX_RS_DIAG_NO_RANK) g = (wx_u32)min((wx_i64)g, a.n - 1);
       if (WX_RS_DIAG_NO_STORE)
         asm volatile("" ::"v"(g), "v"(xk));  // keep the LDS read and the address math
-      else if (WX_RS_NT_STORE)
-        __builtin_nontemporal_store(xk, a.dst_k + g);
       else
-        a.dst_k[g] = xk;
+        a.dst_k[g] = xk;  // plain stores: L2 merges the digit runs' partial lines
       gdst[j] = g;
     }
   }
@@ -731,12 +641,7 @@ __device__ __forceinline__ void wx_rs_payload(const WxRadixPassArgs &a, int tile
 #pragma unroll
   for (int j = 0; j < WX_RS_ITEMS; ++j) {
     const int p = j * WX_RS_BLOCK + threadIdx.x;
-    if (WHOLE || p < tile_n) {
-      if (WX_RS_NT_STORE)
-        __builtin_nontemporal_store(s_k[p], a.dst_v + gdst[j]);
-      else
-        a.dst_v[gdst[j]] = s_k[p];
-    }
+    if (WHOLE || p < tile_n) a.dst_v[gdst[j]] = s_k[p];
   }
 }
 
@@ -811,20 +716,14 @@ __device__ __forceinline__ void wx_radix_tile_body(const WxRadixPassArgs &a, WxR
   wx_rs_rank<KIND, ASC, WHOLE>(a, S, peers, wb, x, rk);
   __syncthreads();
   WX_RS_STAMP(3);
-  if (WX_RS_SPLIT) {
-    const wx_u32 tot = wx_rs_local(a, S, tile);
-    __syncthreads();  // S.ld
-    wx_u64 first = 0ull;
-    if (tid < 256 && tile != 0 && !WX_RS_DIAG_NO_LOOKBACK)
-      first = wx::ld_agent(&a.status[(wx_u64)(tile - 1) * 256 + tid]);  // in flight during the permutation
-    wx_rs_scatter<KIND, ASC, WHOLE>(a, S, wb, x, rk, pos, s_k);
-    if (tid < 256) wx_rs_resolve(a, S, tile, tot, first);
-  } else {
-    wx_rs_digits(a, S, tile);
-    __syncthreads();
-    WX_RS_STAMP(4);
-    wx_rs_scatter<KIND, ASC, WHOLE>(a, S, wb, x, rk, pos, s_k);
-  }
+  const wx_u32 tot = wx_rs_local(a, S, tile);
+  __syncthreads();  // S.ld
+  wx_u64 first[WX_RS_LBW];
+  if (tid < 256 && tile != 0 && !WX_RS_DIAG_NO_LOOKBACK)  // in flight during the permutation
+    wx_rs_walk_first(a, tile, tid, first);
+  WX_RS_STAMP(4);
+  wx_rs_scatter<KIND, ASC, WHOLE>(a, S, wb, x, rk, pos, s_k);
+  if (tid < 256) wx_rs_resolve(a, S, tile, tot, first);
   __syncthreads();
   WX_RS_STAMP(5);
   wx_rs_store<KIND, ASC, WHOLE>(a, S, tile_n, s_k, gdst);
