@@ -20,6 +20,9 @@
 #ifndef WX_UNROLL
 #define WX_UNROLL 8
 #endif
+// K up to this keeps the fully unrolled insertion (C5's K = 5); larger K
+// takes the rolled one (compile time, below)
+#define WX_TOPK_UNROLLED_MAX 8
 #define WX_IDX_NONE 0x7fffffffffffffffll
 
 namespace wx {
@@ -205,6 +208,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
       wx_slow = wx_beats_T && wx_beats_own;
     }
     if (wx_slow) {
+#if WX_TOPK_K <= WX_TOPK_UNROLLED_MAX
 #pragma unroll
       for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
         if (WX_QUAD(wx_u) < wx_nq) {
@@ -219,6 +223,29 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
           }
         }
       }
+#else
+      // large K: the batch's candidate keys first (unrolled), then ONE copy of
+      // the K-deep insertion in a rolled loop (uniform index: the key array
+      // stays in registers) -- 32 inlined copies of a 32-deep insertion took
+      // ~50 s of hiprtc per query shape
+      float wx_fv[WX_UNROLL * 4];
+      wx_u32 wx_pm = 0u;  // bit 4u + e: row (u, e) is a candidate
+#pragma unroll
+      for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
+#pragma unroll
+        for (int wx_e = 0; wx_e < 4; ++wx_e) {
+          WX_COLS(WX_BIND_U)
+          const wx_i64 idx = (WX_QUAD(wx_u) << 2) + wx_e;
+          const bool wx_in = WX_QUAD(wx_u) < wx_nq && idx < wx_a.n_rows && WX_EVAL_COND();
+          const float wx_f = wx_in ? static_cast<float>(WX_EXPR) : 0.0f;
+          wx_fv[wx_u * 4 + wx_e] = wx_f;
+          if (wx_in && !(WX_TOPK_DESC ? wx_f < wx_T : wx_f > wx_T)) wx_pm |= 1u << (wx_u * 4 + wx_e);
+        }
+      }
+#pragma unroll 1
+      for (int wx_r = 0; wx_r < WX_UNROLL * 4; ++wx_r)
+        if ((wx_pm >> wx_r) & 1u) wx_L.offer(wx_fv[wx_r], (WX_QUAD(wx_r >> 2) << 2) + (wx_r & 3));
+#endif
     }
     // after any insert in the wave: the wave's exact K-th best
     if (__builtin_amdgcn_ballot_w64(wx_slow)) {
@@ -278,7 +305,11 @@ extern "C" __global__ __launch_bounds__(WX_FIN_BLOCK) void wx_topk_finalize(WxTo
       ck[b] = c < wx_a.n_cand ? wx_a.cand_k[c] : 0u;
       ci[b] = c < wx_a.n_cand ? wx_a.cand_i[c] : WX_IDX_NONE;
     }
+#if WX_TOPK_K <= WX_TOPK_UNROLLED_MAX
 #pragma unroll
+#else
+#pragma unroll 1
+#endif
     for (int b = 0; b < WX_FIN_BATCH; ++b)
       if (ci[b] != WX_IDX_NONE) L.push(ck[b], ci[b]);
   }
