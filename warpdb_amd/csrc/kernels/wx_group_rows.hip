@@ -7,26 +7,26 @@
 // passing rows' values are put into key-major, row-ordered segments by one
 // stable counting sort straight from the table -- no compaction, no key bits
 // written, no radix passes:
-//   wx_ro_count   (GROUP module)  per static range of whole 16 384-row tiles,
-//                                 the passing rows of each key (bin = key -
-//                                 key_lo), one 2048-bin LDS histogram per range;
+//   wx_ro_count   (GROUP module)  per static range of whole tiles (two
+//                                 ranges per CU), the passing rows of each
+//                                 key (bin = key - key_lo), one 2048-bin LDS
+//                                 histogram per range;
 //   wx_ro_scan / wx_ro_base (util) per-bin totals over the ranges, the bins'
 //                                 exclusive prefix (checked against the
 //                                 ordinary call's group counts), and each
 //                                 range's first output slot of every bin;
-//   wx_ro_scatter (GROUP module)  the range's tiles in order, the next tile's
-//                                 columns in flight: cond / key / value per
-//                                 row, stable in-wave ranks by one returning
-//                                 LDS add per row, the tile's bin prefix, the
-//                                 values permuted into bin order in LDS and
-//                                 written at their segment slots;
+//   wx_ro_scatter (GROUP module)  the range's 8 192-row tiles in order (512
+//                                 threads, two workgroups per CU): cond / key /
+//                                 value per row, stable in-wave ranks by one
+//                                 returning LDS add per row, the tile's bin
+//                                 prefix, the values permuted into bin order
+//                                 in LDS and written at their segment slots;
 //   wx_ro_fold    (util)          one wave per group: the segment's values
-//                                 widened into LDS one 64-value chunk ahead and
-//                                 broadcast back, one dependent double add per
-//                                 row in row order.
-// One persistent 1024-thread workgroup per range: nothing waits on another
-// workgroup.  Wider key spans keep the general path (two ordered
-// compactions + the stable radix pair sort + wx_group_fold).
+//                                 widened into LDS in 64-value chunks (a ring
+//                                 of loads ahead) and broadcast back, one
+//                                 dependent double add per row in row order.
+// Nothing waits on another workgroup.  Wider key spans keep the general path
+// (two ordered compactions + the stable radix pair sort + wx_group_fold).
 
 #define WX_RO_BLOCK 512
 #define WX_RO_WAVES (WX_RO_BLOCK / 64)
@@ -113,6 +113,7 @@ struct WxRoShared {
   // of word [k][d]; then each wave's first tile-local slot of bin d; then,
   // per slot, the output position of the value staged there
   wx_u32 wc[WX_RO_WAVES / 2][WX_RO_BINS];
+  static_assert(WX_RO_WAVES / 2 * WX_RO_BINS >= WX_RO_TILE, "the counters' place holds a position per slot");
   wx_u32 gb[WX_RO_BINS];  // output slot of the tile's first row of bin d, minus its tile-local slot
   wx_u32 ws[WX_RO_WAVES];  // block scan: per-wave sums
 };
