@@ -11,22 +11,23 @@
 // only their 4-byte values and pair sorts their key + payload.
 //
 // wx_radix_hist: one read of the input builds the histograms of all four
-// digits (per-workgroup LDS counters; a wave whose lanes share a digit adds
-// once).  The host scans them into per-digit output bases and skips a pass
-// whose digit is the same for every key.
+// digits (one 1024-thread workgroup per CU, 32 counter copies in LDS).  The
+// host scans them into per-digit output bases and skips a pass whose digit
+// is the same for every key.
 //
-// wx_radix_sweep_* (one pass, "onesweep"): a workgroup takes tile t from a
+// wx_radix_tile_* (one pass, "onesweep"): a workgroup takes tile t from a
 // ticket counter, loads WX_RS_ITEMS keys per lane wave-striped (key i of
 // lane l of wave w at t*TILE + w*64*ITEMS + i*64 + l, so rank order is input
-// order), and ranks each key inside its wave by matching digits with eight
-// ballots: the lowest lane of every digit group bumps the wave's LDS counter
-// and broadcasts the old count.  Threads 0..255 then own one digit each:
-// prefix over the waves, publish the tile's count {A}, look back over the
-// preceding tiles' words of the same digit until an inclusive {P} word, and
-// publish {P}.  Keys are permuted into digit order in LDS and written out
-// from there, so consecutive lanes write consecutive addresses of a digit's
-// run.  Every wait is bounded: a timed-out waiter raises WX_DEVERR_LOOKBACK
-// and the abort word, and the launch drains.
+// order), and ranks each key inside its wave by one returning LDS add on the
+// wave's digit counter (lane 0's digit group by a ballot).  Threads 0..255
+// then own one digit each: prefix over the waves and digits, publish the
+// tile's count {A}; the keys (and payloads) are permuted into digit order in
+// LDS while the digit threads look back over the preceding tiles' words of
+// their digit to an inclusive {P} and publish {P}; the tile is written out
+// of LDS, consecutive lanes to consecutive addresses of a digit's run, with
+// plain stores (L2 merges the runs' partial lines).  Every wait is bounded: a
+// timed-out waiter raises WX_DEVERR_LOOKBACK and the abort word, and the
+// launch drains.
 #define WX_RS_WAVES (WX_RS_BLOCK / 64)
 #ifndef WX_RS_LBW
 // predecessor words per digit per look-back round: keys 3 (11.55 vs 11.71 ms
