@@ -17,7 +17,7 @@ typedef unsigned int wx_u32;
 #define WX_DEVERR_LOOKBACK 1u
 #define WX_DEVERR_CAPACITY 2u
 #define WX_DEVERR_UNSUPPORTED 4u
-#define WX_DEVERR_INTERNAL_KEY 8u  // a partitioned GROUP BY key fell outside its probed range (internal)
+#define WX_DEVERR_INTERNAL_KEY 8u  // GROUP BY consistency check: a key outside its planned range, or counts that disagree
 
 #define WX_OP_DENSE 0
 #define WX_OP_COMPACT 1
