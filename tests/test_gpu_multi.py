@@ -412,3 +412,49 @@ def test_virtual_shards_on_one_device(nshards, monkeypatch, tmp_path):
     assert np.array_equal(rows4, oi4[9:]) and np.array_equal(bits(v4), bits(ov4[9:]))
     r3 = np.asarray(pw.WarpDB.query_multi_gpu_csv(str(path), "price * quantity WHERE price > 15", 1000), np.float32)
     assert np.array_equal(bits(r3), bits(r))
+
+
+def test_timing_read_device_counts_this_devices_timed_launches():
+    # WX_F_TIME launches are summed per process and read (and cleared) per
+    # device with wx_timing_read_device, or all at once with wx_timing_read
+    n = 1_000_003
+    price = torch.empty(n, dtype=torch.float32, device="cuda")
+    L = wx.make_launch(stream=torch.cuda.current_stream().cuda_stream)
+    wx.fill_synthetic(price.data_ptr(), wx.FLOAT32, n, 1, 0, 0.0, 40.0, L)
+    table = wx.Table.from_tensors(price=price)
+    torch.cuda.synchronize()
+    wx.timing_read()  # drop anything earlier tests left
+    Lt = wx.make_launch(stream=torch.cuda.current_stream().cuda_stream, flags=wx.F_TIME)
+    for _ in range(3):
+        wx.reduce_sum(table, "price[idx]", None, Lt)
+    wx.reduce_sum(table, "price[idx]", None, L)  # untimed
+    ms, launches = wx.timing_read(device=torch.cuda.current_device())
+    assert launches == 3 and ms > 0
+    assert wx.timing_read(device=torch.cuda.current_device()) == (0.0, 0)  # read once
+    wx.reduce_sum(table, "price[idx]", None, Lt)
+    ms, launches = wx.timing_read()
+    assert launches == 1 and ms > 0
+
+
+def test_resident_shards_timing(monkeypatch):
+    # ResidentShards.set_timing(kernels, exchange): per-launch kernel time of
+    # every shard's timed launches, and (one-rank RCCL hook) the exchange's
+    # event pairs around collective + merge
+    from warpdb_amd import pywarpdb as pw
+
+    monkeypatch.setenv("WARPDB_EXCHANGE_ONE_RANK", "1")
+    cols = [("price", pw.DataType.Float32, 1, 0, 0.0, 40.0), ("quantity", pw.DataType.Int32, 3, 1, 0, 1023)]
+    rs_ = pw.ResidentShards.synthetic(2_000_003, cols, 1)
+    rs_.sum("(price[idx] * 0.9f)", "(price[idx] > 20.0f)")  # warm (module compiled, buffers sized)
+    rs_.take_timing()
+    rs_.set_timing(True, True)
+    for _ in range(4):
+        rs_.sum("(price[idx] * 0.9f)", "(price[idx] > 20.0f)")
+        rs_.group_sum("price[idx]", "quantity[idx]", "", 0)
+    t = rs_.take_timing()
+    assert t["kernel_ms"] > 0 and t["launches"] >= 8
+    assert t["exchanges"] >= 4 and t["exchange_ms"] >= 0
+    rs_.set_timing(False, False)
+    rs_.sum("(price[idx] * 0.9f)", "(price[idx] > 20.0f)")
+    t = rs_.take_timing()
+    assert t["launches"] == 0 and t["exchanges"] == 0
