@@ -521,6 +521,36 @@ def test_topk_heavy_ties_nan_signed_zero(k, desc):
         assert np.array_equal(bits(keys[:m].cpu().numpy()), bits(rk))
 
 
+@pytest.mark.parametrize("layout", ["one_lane", "sorted", "reverse"])
+@pytest.mark.parametrize("k", [9, 16, 32])
+def test_topk_large_k_spill_paths(k, layout):
+    # K > 8 keeps 8 rows per lane and spills the rest to the wave's list:
+    # the winners packed into one lane's rows (quad q = 5 + 256 u of the first
+    # 2 048-quad span: 32 of them, 16 more in quad 6 + 256 u), every row a new
+    # best (sorted input, descending order) or a new worst (reversed)
+    n = 1_000_003
+    p = synth.uniform_f32(n, 21, 0.0, 40.0)
+    if layout == "one_lane":
+        rows = [4 * (5 + 256 * u) + e for u in range(8) for e in range(4)]
+        rows += [4 * (6 + 256 * u) + e for u in range(4) for e in range(4)]
+        p[np.array(rows)] = np.float32(100.0) + np.arange(len(rows), dtype=np.float32)[::-1]
+    elif layout == "sorted":
+        p = np.sort(p)
+    else:
+        p = np.sort(p)[::-1].copy()
+    cols = {"price": p.astype(np.float32), "quantity": synth.uniform_int(n, 2, 1, 100).astype(np.float32)}
+    table, _ = dev_table(cols)
+    keys = torch.empty(k, device="cuda")
+    idx = torch.empty(k, dtype=torch.int64, device="cuda")
+    for desc in (True, False):
+        for cond, ocond in ((None, None), ("(quantity[idx] > 50.0f)", "quantity > 50")):
+            m = wx.topk(table, "price[idx]", cond, None, k, desc, launch(), keys.data_ptr(), idx.data_ptr())
+            rk, ri, _ = ora.topk(ora.HostTable(cols), "price", k, desc, cond=ocond)
+            assert m == len(rk)
+            assert np.array_equal(idx[:m].cpu().numpy(), ri)
+            assert np.array_equal(bits(keys[:m].cpu().numpy()), bits(rk))
+
+
 def test_topk_fewer_rows_than_k():
     cols = read_csv(os.path.join(GOLDEN, "test.csv"))
     table, _ = dev_table(cols)

@@ -23,6 +23,11 @@
 // K up to this keeps the fully unrolled insertion (C5's K = 5); larger K
 // takes the rolled one (compile time, below)
 #define WX_TOPK_UNROLLED_MAX 8
+// K from this up keeps 8-row lane lists and a spill list per wave (below):
+// 1.95 vs 2.20 ms per 1e9 rows at K = 32, but 1.01 vs 0.80 at K = 9 and
+// 1.17 vs 0.98 at K = 16, where the K-row lane lists' own filter still pays
+// (profiles/r05/topk_by_k.txt)
+#define WX_TOPK_SPILL_MIN 17
 #define WX_IDX_NONE 0x7fffffffffffffffll
 
 namespace wx {
@@ -37,34 +42,55 @@ __device__ __forceinline__ bool better(wx_u32 ka, wx_i64 ia, wx_u32 kb, wx_i64 i
   return ka > kb || (ka == kb && ia < ib);
 }
 
-struct TopList {
-  wx_u32 k[WX_TOPK_K];
-  wx_i64 i[WX_TOPK_K];
-  bool full;  // K real rows held
+template <int C>
+struct TopListT {
+  wx_u32 k[C];
+  wx_i64 i[C];
+  bool full;  // C real rows held
   float wf;   // the worst held key as a float (valid when full)
   __device__ __forceinline__ void init() {
 #pragma unroll
-    for (int j = 0; j < WX_TOPK_K; ++j) { k[j] = 0u; i[j] = WX_IDX_NONE; }
+    for (int j = 0; j < C; ++j) { k[j] = 0u; i[j] = WX_IDX_NONE; }
     full = false;
     wf = 0.0f;
   }
   // Streaming insert of a row whose index exceeds every held index (rows of a
   // thread arrive in increasing order): a tie with the worst key never
-  // enters, so one float compare rejects almost every row.
+  // enters, so one float compare rejects almost every row.  (C = K only: a
+  // full list then holds K better rows, so a rejected row cannot be in the
+  // top K.)
   __device__ __forceinline__ void offer(float f, wx_i64 idx) {
     if (full) {
       const bool in = WX_TOPK_DESC ? (f > wf) : (f < wf);
       if (!in && !(wf != wf && f == f)) return;  // a NaN worst is beaten by any number
     }
     push(rank_of(f), idx);
-    full = i[WX_TOPK_K - 1] != WX_IDX_NONE;
-    wf = key_of(k[WX_TOPK_K - 1]);
+    full = i[C - 1] != WX_IDX_NONE;
+    wf = key_of(k[C - 1]);
+  }
+  // As offer, for a lane list shorter than K: whatever leaves or never
+  // enters the full list -- the evicted worst entry, or the row itself -- is
+  // returned in (sk, si) for the wave's spill list (true when there is one).
+  __device__ __forceinline__ bool offer_spill(float f, wx_i64 idx, wx_u32 &sk, wx_i64 &si) {
+    const wx_u32 r = rank_of(f);
+    if (full && !better(r, idx, k[C - 1], i[C - 1])) {
+      sk = r;
+      si = idx;
+      return true;
+    }
+    const bool ev = full;
+    sk = k[C - 1];
+    si = i[C - 1];
+    push(r, idx);
+    full = i[C - 1] != WX_IDX_NONE;
+    wf = key_of(k[C - 1]);
+    return ev;
   }
   __device__ __forceinline__ void push(wx_u32 key, wx_i64 idx) {
-    if (!better(key, idx, k[WX_TOPK_K - 1], i[WX_TOPK_K - 1])) return;
+    if (!better(key, idx, k[C - 1], i[C - 1])) return;
     bool done = false;
 #pragma unroll
-    for (int j = WX_TOPK_K - 1; j >= 0; --j) {
+    for (int j = C - 1; j >= 0; --j) {
       if (!done) {
         if (j == 0 || !better(key, idx, k[j - 1], i[j - 1])) {
           k[j] = key; i[j] = idx; done = true;
@@ -76,15 +102,17 @@ struct TopList {
   }
   __device__ __forceinline__ void pop() {
 #pragma unroll
-    for (int j = 0; j < WX_TOPK_K - 1; ++j) { k[j] = k[j + 1]; i[j] = i[j + 1]; }
-    k[WX_TOPK_K - 1] = 0u;
-    i[WX_TOPK_K - 1] = WX_IDX_NONE;
+    for (int j = 0; j < C - 1; ++j) { k[j] = k[j + 1]; i[j] = i[j + 1]; }
+    k[C - 1] = 0u;
+    i[C - 1] = WX_IDX_NONE;
   }
 };
+using TopList = TopListT<WX_TOPK_K>;
 
 // Merge the lanes' lists of one wave; lane 0 ends with the wave's K best in
 // out_k/out_i (all lanes compute them).
-__device__ __forceinline__ void wave_merge(TopList &L, wx_u32 (&out_k)[WX_TOPK_K], wx_i64 (&out_i)[WX_TOPK_K]) {
+template <int C>
+__device__ __forceinline__ void wave_merge(TopListT<C> &L, wx_u32 (&out_k)[WX_TOPK_K], wx_i64 (&out_i)[WX_TOPK_K]) {
 #pragma unroll 1
   for (int r = 0; r < WX_TOPK_K; ++r) {
     wx_u32 bk = L.k[0];
@@ -103,8 +131,8 @@ __device__ __forceinline__ void wave_merge(TopList &L, wx_u32 (&out_k)[WX_TOPK_K
 
 // Merge the wave lists of a block through LDS; every thread of wave 0 returns
 // the block's K best (valid in lane 0).
-template <int NW>
-__device__ __forceinline__ void block_merge(TopList &L, wx_u32 (*s_k)[WX_TOPK_K], wx_i64 (*s_i)[WX_TOPK_K],
+template <int NW, int C>
+__device__ __forceinline__ void block_merge(TopListT<C> &L, wx_u32 (*s_k)[WX_TOPK_K], wx_i64 (*s_i)[WX_TOPK_K],
                                             wx_u32 (&bk)[WX_TOPK_K], wx_i64 (&bi)[WX_TOPK_K]) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   wx_u32 wk[WX_TOPK_K];
@@ -126,12 +154,138 @@ __device__ __forceinline__ void block_merge(TopList &L, wx_u32 (*s_k)[WX_TOPK_K]
     wave_merge(M, bk, bi);
   }
 }
+
+#if WX_TOPK_K >= WX_TOPK_SPILL_MIN
+// Large K: each lane streams into a short list (WX_TOPK_LANE entries), and
+// whatever a full lane list evicts or turns away goes to the wave's spill
+// list -- K entries spread over lanes 0..K-1, best first, kept by wave-wide
+// inserts.  A row is dropped only when K better rows are held (a full spill
+// list) or when it is worse than the bound T, so the lanes' lists and the
+// spill list together hold the wave's top K.
+#define WX_TOPK_LANE WX_TOPK_UNROLLED_MAX
+struct SpillList {
+  wx_u32 k = 0u;              // entry `lane` (lanes >= K hold nothing)
+  wx_i64 i = WX_IDX_NONE;
+  // insert (nk, ni) (wave-uniform) in order; the worst entry falls off
+  __device__ __forceinline__ void insert(wx_u32 nk, wx_i64 ni) {
+    const int lane = threadIdx.x & 63;
+    const bool ahead = lane < WX_TOPK_K && better(k, i, nk, ni);
+    const int pos = __builtin_popcountll(__builtin_amdgcn_ballot_w64(ahead));  // the ahead entries are a prefix
+    const wx_u32 pk = __shfl_up(k, 1);
+    const wx_i64 pi = __shfl_up(i, 1);
+    if (pos < WX_TOPK_K && lane < WX_TOPK_K) {
+      if (lane == pos) { k = nk; i = ni; }
+      else if (lane > pos) { k = pk; i = pi; }
+    }
+  }
+  // every lane's pending spill (sp: it has one), in lane order
+  __device__ __forceinline__ void take(bool sp, wx_u32 sk, wx_i64 si) {
+    wx_u64 m = __builtin_amdgcn_ballot_w64(sp);
+    while (m) {
+      const int src = __builtin_ctzll(m);
+      m &= m - 1;
+      const wx_u32 nk = (wx_u32)__builtin_amdgcn_readlane((int)sk, src);
+      const wx_u32 lo = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)(wx_u64)si, src);
+      const wx_u32 hi = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)((wx_u64)si >> 32), src);
+      insert(nk, (wx_i64)(((wx_u64)hi << 32) | lo));
+    }
+  }
+  // the K-th entry's rank (0: fewer than K held)
+  __device__ __forceinline__ wx_u32 kth() const {
+    const wx_u32 r = (wx_u32)__builtin_amdgcn_readlane((int)k, WX_TOPK_K - 1);
+    const wx_u32 lo = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)(wx_u64)i, WX_TOPK_K - 1);
+    const wx_u32 hi = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)((wx_u64)i >> 32), WX_TOPK_K - 1);
+    return (((wx_u64)hi << 32) | lo) != (wx_u64)WX_IDX_NONE ? r : 0u;
+  }
+};
+// The wave's K-th best (rank, 0 when it holds fewer than K rows): K rounds
+// of a wave arg-max over the lanes' lists, popping the winner, keeping only
+// the last round (no K-entry arrays).
+template <int C>
+__device__ __forceinline__ wx_u32 wave_kth(TopListT<C> L) {
+  wx_u32 bk = 0u;
+  wx_i64 bi = WX_IDX_NONE;
+#pragma unroll 1
+  for (int r = 0; r < WX_TOPK_K; ++r) {
+    bk = L.k[0];
+    bi = L.i[0];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const wx_u32 ok = __shfl_xor(bk, o);
+      const wx_i64 oi = __shfl_xor(bi, o);
+      if (better(ok, oi, bk, bi)) { bk = ok; bi = oi; }
+    }
+    if (L.i[0] == bi && L.k[0] == bk && bi != WX_IDX_NONE) L.pop();
+  }
+  return bi != WX_IDX_NONE ? bk : 0u;
+}
+
+// The block's K best into cand_k / cand_i[0, K): each wave writes its K best
+// (K rounds of a wave arg-max) to LDS, then every entry of the NW sorted
+// lists takes its place = the entries that beat it (its own list's by
+// position, the others' by counting); places < K are written.  No K-entry
+// register arrays.
+template <int NW, int C>
+__device__ __forceinline__ void block_place(TopListT<C> &L, wx_u32 (*s_k)[WX_TOPK_K], wx_i64 (*s_i)[WX_TOPK_K],
+                                            wx_u32 *cand_k, wx_i64 *cand_i) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll 1
+  for (int r = 0; r < WX_TOPK_K; ++r) {
+    wx_u32 bk = L.k[0];
+    wx_i64 bi = L.i[0];
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const wx_u32 ok = __shfl_xor(bk, o);
+      const wx_i64 oi = __shfl_xor(bi, o);
+      if (better(ok, oi, bk, bi)) { bk = ok; bi = oi; }
+    }
+    if (lane == 0) { s_k[wave][r] = bk; s_i[wave][r] = bi; }
+    if (L.i[0] == bi && L.k[0] == bk && bi != WX_IDX_NONE) L.pop();
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NW * WX_TOPK_K; e += NW * 64) {
+    const int w = e / WX_TOPK_K, r = e % WX_TOPK_K;
+    const wx_u32 k = s_k[w][r];
+    const wx_i64 i = s_i[w][r];
+    if (i == WX_IDX_NONE) continue;  // empty tail entries: the slots they would take stay empty below
+    int place = r;
+    for (int v = 0; v < NW; ++v) {
+      if (v == w) continue;
+      for (int q = 0; q < WX_TOPK_K; ++q) place += better(s_k[v][q], s_i[v][q], k, i) ? 1 : 0;
+    }
+    if (place < WX_TOPK_K) { cand_k[place] = k; cand_i[place] = i; }
+  }
+  // slots past the block's valid entries: empty
+  int nvalid = 0;
+  for (int v = 0; v < NW; ++v)
+    for (int q = 0; q < WX_TOPK_K; ++q) nvalid += s_i[v][q] != WX_IDX_NONE ? 1 : 0;
+  for (int j = nvalid + (int)threadIdx.x; j < WX_TOPK_K; j += NW * 64) { cand_k[j] = 0u; cand_i[j] = WX_IDX_NONE; }
+}
+
+// the lane list plus this lane's spill entry, for the wave merges
+__device__ __forceinline__ TopListT<WX_TOPK_LANE + 1> with_spill(const TopListT<WX_TOPK_LANE> &L, const SpillList &W) {
+  TopListT<WX_TOPK_LANE + 1> M;
+#pragma unroll
+  for (int j = 0; j < WX_TOPK_LANE; ++j) { M.k[j] = L.k[j]; M.i[j] = L.i[j]; }
+  M.k[WX_TOPK_LANE] = 0u;
+  M.i[WX_TOPK_LANE] = WX_IDX_NONE;
+  M.full = false;
+  M.wf = 0.0f;
+  if (W.i != WX_IDX_NONE) M.push(W.k, W.i);
+  return M;
+}
+#endif
 }  // namespace wx
 
 extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs wx_a) {
   __shared__ wx_u32 s_k[WX_WAVES][WX_TOPK_K];
   __shared__ wx_i64 s_i[WX_WAVES][WX_TOPK_K];
+#if WX_TOPK_K < WX_TOPK_SPILL_MIN
   wx::TopList wx_L;
+#else
+  wx::TopListT<WX_TOPK_LANE> wx_L;  // + the wave's spill list (large K)
+  wx::SpillList wx_W;
+#endif
   wx_L.init();
   // Batches of WX_UNROLL row quads per thread.  Once the lane's list is full
   // (and its worst key is a number), a complete batch costs one max/min of its
@@ -203,10 +357,17 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
         }
       }
       const bool wx_beats_T = wx_T == wx_none || (WX_TOPK_DESC ? wx_m >= wx_T : wx_m <= wx_T);
+#if WX_TOPK_K < WX_TOPK_SPILL_MIN
       const bool wx_beats_own =
           !wx_L.full || wx_L.wf != wx_L.wf || (WX_TOPK_DESC ? wx_m > wx_L.wf : wx_m < wx_L.wf);
       wx_slow = wx_beats_T && wx_beats_own;
+#else
+      wx_slow = wx_beats_T;  // a short lane list turns nothing away: rows it cannot keep spill
+#endif
     }
+#if WX_TOPK_K >= WX_TOPK_SPILL_MIN
+    wx_slow = __builtin_amdgcn_ballot_w64(wx_slow) != 0ull;  // the spill inserts need the whole wave
+#endif
     if (wx_slow) {
 #if WX_TOPK_K <= WX_TOPK_UNROLLED_MAX
 #pragma unroll
@@ -242,18 +403,38 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
           if (wx_in && !(WX_TOPK_DESC ? wx_f < wx_T : wx_f > wx_T)) wx_pm |= 1u << (wx_u * 4 + wx_e);
         }
       }
+#if WX_TOPK_K < WX_TOPK_SPILL_MIN
 #pragma unroll 1
       for (int wx_r = 0; wx_r < WX_UNROLL * 4; ++wx_r)
         if ((wx_pm >> wx_r) & 1u) wx_L.offer(wx_fv[wx_r], (WX_QUAD(wx_r >> 2) << 2) + (wx_r & 3));
+#else
+#pragma unroll 1
+      for (int wx_r = 0; wx_r < WX_UNROLL * 4; ++wx_r) {
+        bool wx_sp = false;
+        wx_u32 wx_sk = 0u;
+        wx_i64 wx_si = WX_IDX_NONE;
+        if ((wx_pm >> wx_r) & 1u) {
+          wx_sp = wx_L.offer_spill(wx_fv[wx_r], (WX_QUAD(wx_r >> 2) << 2) + (wx_r & 3), wx_sk, wx_si);
+          const float wx_sf = wx::key_of(wx_sk);
+          if (wx_sp && (WX_TOPK_DESC ? wx_sf < wx_T : wx_sf > wx_T)) wx_sp = false;  // strictly worse than T
+        }
+        wx_W.take(wx_sp, wx_sk, wx_si);  // wave-uniform: every lane runs the loop
+      }
+#endif
 #endif
     }
     // after any insert in the wave: the wave's exact K-th best
     if (__builtin_amdgcn_ballot_w64(wx_slow)) {
+#if WX_TOPK_K < WX_TOPK_SPILL_MIN
       wx::TopList wx_c = wx_L;
       wx_u32 wk[WX_TOPK_K];
       wx_i64 wi[WX_TOPK_K];
       wx::wave_merge(wx_c, wk, wi);
       const wx_u32 r = wi[WX_TOPK_K - 1] != WX_IDX_NONE ? wk[WX_TOPK_K - 1] : 0u;  // 0: fewer than K rows, or NaN
+#else
+      // the wave's held rows: lane lists + spill list
+      const wx_u32 r = wx::wave_kth(wx::with_spill(wx_L, wx_W));
+#endif
       if (r > wx_pub) {
         const float t = wx::key_of(r);
         wx_T = WX_TOPK_DESC ? fmaxf(wx_T, t) : fminf(wx_T, t);
@@ -268,6 +449,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
       }
     }
   }
+#if WX_TOPK_K < WX_TOPK_SPILL_MIN
   wx_u32 bk[WX_TOPK_K];
   wx_i64 bi[WX_TOPK_K];
   wx::block_merge<WX_WAVES>(wx_L, s_k, s_i, bk, bi);
@@ -278,6 +460,11 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
       wx_a.cand_i[(wx_i64)blockIdx.x * WX_TOPK_K + j] = bi[j];
     }
   }
+#else
+  auto wx_c = wx::with_spill(wx_L, wx_W);
+  wx::block_place<WX_WAVES>(wx_c, s_k, s_i, wx_a.cand_k + (wx_i64)blockIdx.x * WX_TOPK_K,
+                            wx_a.cand_i + (wx_i64)blockIdx.x * WX_TOPK_K);
+#endif
 }
 
 // One 1024-thread block; candidate loads are issued 8 per thread at a time
