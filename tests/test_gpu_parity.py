@@ -551,6 +551,53 @@ def test_topk_large_k_spill_paths(k, layout):
             assert np.array_equal(bits(keys[:m].cpu().numpy()), bits(rk))
 
 
+@pytest.mark.parametrize("data", ["ties", "nan", "sorted"])
+@pytest.mark.parametrize("k", [1, 5, 32])
+def test_topk_seed_pass(k, data, monkeypatch):
+    # WX_TOPK_SEED=2 forces the seed pass (wx_topk_seed + a seed finalize into
+    # bound slot 0) on a table below its default 2^24 rows.  Heavy ties: the
+    # seed equals the winners' key, and the winners are the smallest row
+    # indices among thousands of equal keys, most of them outside the sample.
+    monkeypatch.setenv("WARPDB_EXTRA_DEFINES", "WX_TOPK_SEED=2")
+    n = 300_003
+    p = synth.uniform_f32(n, 33, 0.0, 40.0)
+    if data == "ties":
+        p = (np.round(p * 2.0) / 2.0).astype(np.float32)
+    elif data == "nan":
+        p[::7] = np.float32("nan")
+        p[1::11] = np.float32(-0.0)
+    else:
+        p = np.sort(p)
+    cols = {"price": p.astype(np.float32), "quantity": synth.uniform_int(n, 3, 1, 100).astype(np.float32)}
+    table, _ = dev_table(cols)
+    keys = torch.empty(k, device="cuda")
+    idx = torch.empty(k, dtype=torch.int64, device="cuda")
+    for desc in (True, False):
+        for cond, ocond in ((None, None), ("(quantity[idx] > 50.0f)", "quantity > 50")):
+            m = wx.topk(table, "price[idx]", cond, None, k, desc, launch(), keys.data_ptr(), idx.data_ptr())
+            rk, ri, _ = ora.topk(ora.HostTable(cols), "price", k, desc, cond=ocond)
+            assert m == len(rk)
+            assert np.array_equal(idx[:m].cpu().numpy(), ri)
+            assert np.array_equal(bits(keys[:m].cpu().numpy()), bits(rk))
+
+
+def test_topk_seed_pass_default_size():
+    # the default seed rule (K > 8 over tables of 2^24 rows and more), ties at
+    # the winners
+    n = (1 << 24) + 5
+    p = (np.round(synth.uniform_f32(n, 34, 0.0, 40.0) * 4.0) / 4.0).astype(np.float32)
+    cols = {"price": p}
+    table, _ = dev_table(cols)
+    keys = torch.empty(32, device="cuda")
+    idx = torch.empty(32, dtype=torch.int64, device="cuda")
+    for k, desc in ((9, True), (32, False)):
+        m = wx.topk(table, "price[idx]", None, None, k, desc, launch(), keys.data_ptr(), idx.data_ptr())
+        rk, ri, _ = ora.topk(ora.HostTable(cols), "price", k, desc)
+        assert m == len(rk) == k
+        assert np.array_equal(idx[:m].cpu().numpy(), ri)
+        assert np.array_equal(bits(keys[:m].cpu().numpy()), bits(rk))
+
+
 def test_topk_fewer_rows_than_k():
     cols = read_csv(os.path.join(GOLDEN, "test.csv"))
     table, _ = dev_table(cols)

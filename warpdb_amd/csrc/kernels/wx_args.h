@@ -40,6 +40,7 @@ typedef unsigned int wx_u32;
 #define WX_TOPK_MAX 32
 #define WX_TOPK_SLOTS 64        // top-K grid-wide bound: one slot per wave lane
 #define WX_TOPK_SLOT_STRIDE 64  // u32 elements between slots (256 B)
+#define WX_TOPK_SEED_SPANS 128  // top-K seed pass: workgroups, one 8 192-row span each (~1M rows)
 #define WX_SORT_LDS (WX_BLOCK * 8)
 // LSD radix sort (wx_radix_*): 8-bit digits, 4 passes over 32-bit keys;
 // one tile = WX_RS_BLOCK threads x WX_RS_ITEMS keys, one 64-bit look-back
@@ -277,6 +278,8 @@ struct WxTopkArgs {
   wx_i64 *cand_i;    // [gridDim.x * K]
   wx_u32 *g_thresh;  // [WX_TOPK_SLOTS * WX_TOPK_SLOT_STRIDE] lower bounds on the K-th best rank (0 = none), zeroed per call
   wx_i64 n_rows;
+  wx_i64 q_stride;   // row quads between consecutive workgroups' first spans (the scan: one span)
+  wx_i64 q_step;     // row quads a workgroup advances per batch (the scan: gridDim.x spans)
 };
 
 struct WxTopkFinArgs {
@@ -290,6 +293,7 @@ struct WxTopkFinArgs {
   float *out_vals;
   wx_i64 *count_out;
   wx_u32 *g_thresh;  // the scan's grid-wide bound slots: zeroed here for the next query
+  int seed;          // 1: the seed pass -- raise slot 0 to the K-th best rank, keep the slots, no outputs
 };
 
 struct WxFillArgs {

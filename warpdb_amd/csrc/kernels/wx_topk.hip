@@ -178,9 +178,19 @@ struct SpillList {
       else if (lane > pos) { k = pk; i = pi; }
     }
   }
-  // every lane's pending spill (sp: it has one), in lane order
+  // (sk, si) would enter: the list is short, or it beats the K-th entry
+  __device__ __forceinline__ bool enters(wx_u32 sk, wx_i64 si) const {
+    const wx_u32 kk = (wx_u32)__builtin_amdgcn_readlane((int)k, WX_TOPK_K - 1);
+    const wx_u32 lo = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)(wx_u64)i, WX_TOPK_K - 1);
+    const wx_u32 hi = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)((wx_u64)i >> 32), WX_TOPK_K - 1);
+    const wx_i64 ki = (wx_i64)(((wx_u64)hi << 32) | lo);
+    return ki == WX_IDX_NONE || better(sk, si, kk, ki);
+  }
+  // every lane's pending spill (sp: it has one), in lane order; a spill the
+  // K-th entry already beats is dropped before its turn (the serial inserts
+  // are the slow batches' cost: a first batch spills ~24 rows per lane)
   __device__ __forceinline__ void take(bool sp, wx_u32 sk, wx_i64 si) {
-    wx_u64 m = __builtin_amdgcn_ballot_w64(sp);
+    wx_u64 m = __builtin_amdgcn_ballot_w64(sp && enters(sk, si));
     while (m) {
       const int src = __builtin_ctzll(m);
       m &= m - 1;
@@ -188,6 +198,7 @@ struct SpillList {
       const wx_u32 lo = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)(wx_u64)si, src);
       const wx_u32 hi = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)((wx_u64)si >> 32), src);
       insert(nk, (wx_i64)(((wx_u64)hi << 32) | lo));
+      if (m) m &= __builtin_amdgcn_ballot_w64(enters(sk, si));
     }
   }
   // the K-th entry's rank (0: fewer than K held)
@@ -277,7 +288,7 @@ __device__ __forceinline__ TopListT<WX_TOPK_LANE + 1> with_spill(const TopListT<
 #endif
 }  // namespace wx
 
-extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs wx_a) {
+__device__ __forceinline__ void wx_topk_scan_body(const WxTopkArgs &wx_a) {
   __shared__ wx_u32 s_k[WX_WAVES][WX_TOPK_K];
   __shared__ wx_i64 s_i[WX_WAVES][WX_TOPK_K];
 #if WX_TOPK_K < WX_TOPK_SPILL_MIN
@@ -301,7 +312,8 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
   // bound lives in WX_TOPK_SLOTS slots on separate 256-B lines (a single
   // address serialised ≈50K early atomics: 2.4 ms); a wave publishes to its
   // workgroup's slot and every 8th batch reads all slots with one vector load
-  // (lane l: slot l) and a wave max (relaxed: a stale value is still a bound).
+  // (lane l: slot l) and a wave max (relaxed: a stale value is still a bound),
+  // the first time before batch 0 (the seed pass may have raised them).
   const float wx_none = WX_TOPK_DESC ? -__builtin_inff() : __builtin_inff();
   float wx_T = wx_none;   // best known bound (this wave and the grid)
   wx_u32 wx_pub = 0u;     // best rank this wave has found
@@ -309,7 +321,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
   int wx_batch = 0;
   const wx_i64 wx_nq = (wx_a.n_rows + 3) >> 2;
   const wx_i64 wx_nfull = wx_a.n_rows >> 2;
-  for (wx_i64 wx_base = (wx_i64)blockIdx.x * WX_SPAN; wx_base < wx_nq; wx_base += (wx_i64)gridDim.x * WX_SPAN) {
+  for (wx_i64 wx_base = (wx_i64)blockIdx.x * wx_a.q_stride; wx_base < wx_nq; wx_base += wx_a.q_step) {
     WX_COLS(WX_DECL_U)
     const bool wx_whole = WX_ALIGNED16 && wx_base + WX_SPAN <= wx_nfull;  // workgroup-uniform
     if (wx_whole) {
@@ -325,7 +337,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
         WX_COLS(WX_LOAD_U)
       }
     }
-    if ((wx_batch++ & 7) == 7) {
+    if ((wx_batch++ & 7) == 0) {
       wx_u32 wx_g = __hip_atomic_load(wx_a.g_thresh + (threadIdx.x & 63) * WX_TOPK_SLOT_STRIDE, __ATOMIC_RELAXED,
                                       __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
@@ -467,6 +479,18 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
 #endif
 }
 
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs wx_a) { wx_topk_scan_body(wx_a); }
+
+// The seed pass (tables of 2^24 rows and more, warpexec.cpp do_topk): the
+// same scan over one span per workgroup at evenly spaced offsets (about 1M
+// rows), merged by wx_topk_finalize with seed = 1 into slot 0 before the scan
+// starts.  Without it a wave's bound is the K-th best of the rows IT has seen
+// (and the grid's the best such), which turns batches away only after ~K
+// batches; the seed's K-th best of 1M rows is a bound from batch 0 on.  Exact:
+// it is the key of a real row with K rows at least as good (the scan drops
+// only rows strictly worse).  Its own name keeps it apart in kernel traces.
+extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_seed(WxTopkArgs wx_a) { wx_topk_scan_body(wx_a); }
+
 // One 1024-thread block; candidate loads are issued 8 per thread at a time
 // (the loop is latency-bound otherwise: the candidates sit in other XCDs' L2).
 #define WX_FIN_BLOCK 1024
@@ -474,7 +498,7 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_topk_scan(WxTopkArgs w
 extern "C" __global__ __launch_bounds__(WX_FIN_BLOCK) void wx_topk_finalize(WxTopkFinArgs wx_a) {
   // the scan has finished (stream order): reset its bound slots for the next
   // query here instead of a host memset per query
-  if (wx_a.g_thresh && threadIdx.x < WX_TOPK_SLOTS)
+  if (wx_a.g_thresh && !wx_a.seed && threadIdx.x < WX_TOPK_SLOTS)
     __hip_atomic_store(wx_a.g_thresh + threadIdx.x * WX_TOPK_SLOT_STRIDE, 0u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
   __shared__ wx_u32 s_k[WX_FIN_BLOCK / 64][WX_TOPK_K];
@@ -512,7 +536,10 @@ extern "C" __global__ __launch_bounds__(WX_FIN_BLOCK) void wx_topk_finalize(WxTo
       n += bi[j] != WX_IDX_NONE ? 1 : 0;
     }
     if (wx_a.count_out) *wx_a.count_out = n;
+    if (wx_a.seed && bi[WX_TOPK_K - 1] != WX_IDX_NONE)  // K rows: the K-th best rank bounds the table's
+      atomicMax(wx_a.g_thresh, bk[WX_TOPK_K - 1]);
   }
+  if (wx_a.seed) return;
   __syncthreads();
   const int wx_j = threadIdx.x;
   if (wx_j < WX_TOPK_K && s_bi[wx_j] != WX_IDX_NONE) {
