@@ -505,14 +505,13 @@ def test_stream_comm_fallback_is_collective(monkeypatch):
     from warpdb_amd import _warpcomm as wc
     from warpdb_amd import distributed as wd
 
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    for k, v in {"MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "WORLD_SIZE": "1", "RANK": "0",
-                 "WARPDB_EXCHANGE_ONE_RANK": "1"}.items():
+    for k, v in {"MASTER_ADDR": "127.0.0.1", "WORLD_SIZE": "1", "RANK": "0", "WARPDB_EXCHANGE_ONE_RANK": "1"}.items():
         monkeypatch.setenv(k, v)
     torch.cuda.set_device(0)
-    dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    # the store binds its own free port (a probed port can be taken by another
+    # process before the store listens: EADDRINUSE once on a shared box)
+    store = dist.TCPStore("127.0.0.1", 0, 1, is_master=True)
+    dist.init_process_group("nccl", store=store, rank=0, world_size=1, device_id=torch.device("cuda", 0))
     try:
         def broken():
             raise RuntimeError("no id for this test")
