@@ -291,6 +291,9 @@ __device__ __forceinline__ TopListT<WX_TOPK_LANE + 1> with_spill(const TopListT<
 __device__ __forceinline__ void wx_topk_scan_body(const WxTopkArgs &wx_a) {
   __shared__ wx_u32 s_k[WX_WAVES][WX_TOPK_K];
   __shared__ wx_i64 s_i[WX_WAVES][WX_TOPK_K];
+#if WX_TOPK_K > WX_TOPK_UNROLLED_MAX
+  __shared__ float wx_s_fv[WX_UNROLL * 4][WX_BLOCK];  // a slow batch's candidate keys (each thread its own column)
+#endif
 #if WX_TOPK_K < WX_TOPK_SPILL_MIN
   wx::TopList wx_L;
 #else
@@ -401,7 +404,9 @@ __device__ __forceinline__ void wx_topk_scan_body(const WxTopkArgs &wx_a) {
       // the K-deep insertion in a rolled loop (uniform index: the key array
       // stays in registers) -- 32 inlined copies of a 32-deep insertion took
       // ~50 s of hiprtc per query shape
-      float wx_fv[WX_UNROLL * 4];
+      // the candidate keys staged in LDS (column r, lane tid: conflict-free): a
+      // register array indexed by the rolled loop below lived in scratch
+      float (*wx_fv)[WX_BLOCK] = wx_s_fv;
       wx_u32 wx_pm = 0u;  // bit 4u + e: row (u, e) is a candidate
 #pragma unroll
       for (int wx_u = 0; wx_u < WX_UNROLL; ++wx_u) {
@@ -411,14 +416,14 @@ __device__ __forceinline__ void wx_topk_scan_body(const WxTopkArgs &wx_a) {
           const wx_i64 idx = (WX_QUAD(wx_u) << 2) + wx_e;
           const bool wx_in = WX_QUAD(wx_u) < wx_nq && idx < wx_a.n_rows && WX_EVAL_COND();
           const float wx_f = wx_in ? static_cast<float>(WX_EXPR) : 0.0f;
-          wx_fv[wx_u * 4 + wx_e] = wx_f;
+          wx_fv[wx_u * 4 + wx_e][threadIdx.x] = wx_f;
           if (wx_in && !(WX_TOPK_DESC ? wx_f < wx_T : wx_f > wx_T)) wx_pm |= 1u << (wx_u * 4 + wx_e);
         }
       }
 #if WX_TOPK_K < WX_TOPK_SPILL_MIN
 #pragma unroll 1
       for (int wx_r = 0; wx_r < WX_UNROLL * 4; ++wx_r)
-        if ((wx_pm >> wx_r) & 1u) wx_L.offer(wx_fv[wx_r], (WX_QUAD(wx_r >> 2) << 2) + (wx_r & 3));
+        if ((wx_pm >> wx_r) & 1u) wx_L.offer(wx_fv[wx_r][threadIdx.x], (WX_QUAD(wx_r >> 2) << 2) + (wx_r & 3));
 #else
 #pragma unroll 1
       for (int wx_r = 0; wx_r < WX_UNROLL * 4; ++wx_r) {
@@ -426,7 +431,7 @@ __device__ __forceinline__ void wx_topk_scan_body(const WxTopkArgs &wx_a) {
         wx_u32 wx_sk = 0u;
         wx_i64 wx_si = WX_IDX_NONE;
         if ((wx_pm >> wx_r) & 1u) {
-          wx_sp = wx_L.offer_spill(wx_fv[wx_r], (WX_QUAD(wx_r >> 2) << 2) + (wx_r & 3), wx_sk, wx_si);
+          wx_sp = wx_L.offer_spill(wx_fv[wx_r][threadIdx.x], (WX_QUAD(wx_r >> 2) << 2) + (wx_r & 3), wx_sk, wx_si);
           const float wx_sf = wx::key_of(wx_sk);
           if (wx_sp && (WX_TOPK_DESC ? wx_sf < wx_T : wx_sf > wx_T)) wx_sp = false;  // strictly worse than T
         }
