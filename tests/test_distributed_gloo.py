@@ -351,3 +351,17 @@ def test_shard_range_matches_plan():
         plan = [(b, e) for _, b, e in pw.plan_shards(n, w)]
         ranges = [wd.shard_range(n, w, r) for r in range(w)]
         assert [r for r in ranges if r[0] < r[1]] == plan
+
+
+def test_enable_stream_comm_without_process_group():
+    """with no process group initialised, the public
+    enable_stream_comm returns False (nothing to exchange over) instead of
+    raising from torch's default-group lookup."""
+    import torch.distributed as dist
+
+    from warpdb_amd import distributed as wd
+
+    if dist.is_initialized():
+        pytest.skip("a process group is initialised in this process")
+    assert wd.enable_stream_comm() is False
+    assert wd.stream_comm() is None

@@ -157,6 +157,20 @@ def test_cpp_frontend_binary():
     assert "frontend_test: all passed" in r.stdout
 
 
+def test_boundary_layout_static_asserts():
+    # tests/cpp/layout_test.cpp: the source-level compatibility INTEGRATION.md
+    # 1.1 states (64-bit row counts, DataType == wx_dtype numbering, the
+    # reference's constructor calls) pinned by static_assert; building it is the test
+    import subprocess
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run(["make", "-s", "-C", os.path.join(root, "tests", "cpp"), "layout_test"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    r = subprocess.run([os.path.join(root, "tests", "cpp", "bin", "layout_test")], capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+
+
 def test_host_code_under_asan_ubsan():
     # tests/cpp/sanitize_test.cpp: the front end on random token soup and deep
     # nesting, the parallel CSV parser against a sequential reading, built with

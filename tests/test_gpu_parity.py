@@ -917,3 +917,81 @@ def test_concurrent_streams_from_threads():
     for t in th:
         t.join()
     assert not errors, errors
+
+
+def test_workspace_growth_on_fresh_stream_under_load():
+    """A fresh stream's workspace is created and grown (look-back status
+    words, tickets, radix status) while three other streams keep the GPU busy
+    and the null stream is held by a spin kernel.  The zero-fills of fresh
+    workspace buffers must be ordered before the first kernel that reads them
+    (warpexec.cpp `ensure`: hipMemsetAsync on the workspace stream; the
+    round-5 abort came from null-stream fills)."""
+    import threading
+
+    stop = threading.Event()
+    errors = []
+
+    def busy(j):
+        n = 4_000_000 + 17 * j
+        price = torch.empty(n, dtype=torch.float32, device="cuda")
+        qty = torch.empty(n, dtype=torch.float32, device="cuda")
+        L0 = launch()
+        wx.fill_synthetic(price.data_ptr(), wx.FLOAT32, n, 300 + j, 0, 0.0, 40.0, L0)
+        wx.fill_synthetic(qty.data_ptr(), wx.FLOAT32, n, 400 + j, 1, 1, 100, L0)
+        torch.cuda.synchronize()
+        table = wx.Table(n, [wx.Column("price", wx.FLOAT32, price.data_ptr()),
+                             wx.Column("quantity", wx.FLOAT32, qty.data_ptr())])
+        want = int((price > 10.0).sum())
+        vals = torch.empty(n, device="cuda")
+        idx = torch.empty(n, dtype=torch.int64, device="cuda")
+        stream = torch.cuda.Stream()
+        try:
+            with torch.cuda.stream(stream):
+                L = wx.make_launch(device=0, stream=stream.cuda_stream, flags=wx.F_SYNC)
+                while not stop.is_set():
+                    cnt = wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 10.0f)", L,
+                                            wx.MODE_COMPACT, vals.data_ptr(), idx.data_ptr(), 8, 0, want_count=True)
+                    assert cnt == want
+                stream.synchronize()
+        except Exception as e:  # noqa: BLE001 - reported by the main thread
+            errors.append(("busy", j, repr(e)))
+
+    th = [threading.Thread(target=busy, args=(j,)) for j in range(3)]
+    for t in th:
+        t.start()
+    try:
+        for rep, n in enumerate([100_003, 1_000_003, 4_000_037, 9_000_011]):
+            price = torch.empty(n, dtype=torch.float32, device="cuda")
+            qty = torch.empty(n, dtype=torch.float32, device="cuda")
+            L0 = launch()
+            wx.fill_synthetic(price.data_ptr(), wx.FLOAT32, n, 500 + rep, 0, 0.0, 40.0, L0)
+            wx.fill_synthetic(qty.data_ptr(), wx.FLOAT32, n, 600 + rep, 1, 1, 100, L0)
+            torch.cuda.synchronize()
+            table = wx.Table(n, [wx.Column("price", wx.FLOAT32, price.data_ptr()),
+                                 wx.Column("quantity", wx.FLOAT32, qty.data_ptr())])
+            mask = price > 15.0
+            want_idx = torch.nonzero(mask).flatten()
+            want_vals = (price * qty)[mask]
+            want_sorted = torch.sort(price).values
+            # a fresh stream per size: a new workspace, grown on its first use
+            stream = torch.cuda.Stream()
+            vals = torch.empty(n, device="cuda")
+            idx = torch.empty(n, dtype=torch.int64, device="cuda")
+            keys = price.clone()
+            torch.cuda.synchronize()
+            torch.cuda._sleep(50_000_000)  # hold the null stream (~20-50 ms)
+            with torch.cuda.stream(stream):
+                L = wx.make_launch(device=0, stream=stream.cuda_stream, flags=wx.F_SYNC)
+                cnt = wx.project_filter(table, "(price[idx] * quantity[idx])", "(price[idx] > 15.0f)", L,
+                                        wx.MODE_COMPACT, vals.data_ptr(), idx.data_ptr(), 8, 0, want_count=True)
+                wx.sort_float(keys.data_ptr(), n, True, L)
+                stream.synchronize()
+            torch.cuda.synchronize()
+            assert cnt == want_idx.numel(), (n, cnt)
+            assert torch.equal(idx[:cnt], want_idx) and torch.equal(vals[:cnt], want_vals), n
+            assert torch.equal(keys, want_sorted), n
+    finally:
+        stop.set()
+        for t in th:
+            t.join()
+    assert not errors, errors

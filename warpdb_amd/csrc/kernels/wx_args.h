@@ -18,6 +18,13 @@ typedef unsigned int wx_u32;
 #define WX_DEVERR_CAPACITY 2u
 #define WX_DEVERR_UNSUPPORTED 4u
 #define WX_DEVERR_INTERNAL_KEY 8u  // GROUP BY consistency check: a key outside its planned range, or counts that disagree
+// Look-back abort report, workspace ctrs[WX_LBD_BASE ..  + 4]: [0] claim (the
+// first aborting waiter sets it and fills the rest), [1] kind | launch epoch
+// << 8 | digit << 16 | pass << 32, [2] the waiting tile, [3] the tile it
+// waited on, [4] that tile's status word as last seen.  Cleared by the host.
+#define WX_LBD_BASE 3
+#define WX_LBD_COMPACT 1u
+#define WX_LBD_RADIX 2u
 
 #define WX_OP_DENSE 0
 #define WX_OP_COMPACT 1
@@ -67,7 +74,7 @@ struct WxCompactArgs {
   float *out_val;     // nullable
   void *out_idx;      // nullable; int32 or int64
   wx_u64 *status;     // [n_tiles + 1] {epoch:6 | flag:2 | value:56}; [n_tiles] = abort word
-  wx_u64 *ctrs;       // [0] tile ticket, [1] error bits, [2] retired workgroups (0 between launches)
+  wx_u64 *ctrs;       // [0] tile ticket, [1] error bits, [2] retired workgroups (0 between launches), [3..7] WX_LBD_*
   wx_i64 *count_out;  // nullable
   wx_i64 n_rows;
   wx_i64 n_tiles;
@@ -394,6 +401,7 @@ struct WxRadixPassArgs {
   wx_u64 *status;            // [n_tiles][256] look-back words {epoch:6 | flag:2 | count:56}
   wx_u32 *ctl;               // [0] tile ticket, [1] abort word
   wx_u32 *err;               // sticky device error bits (workspace ctrs[1])
+  wx_u64 *lbd;               // look-back abort report (workspace ctrs[WX_LBD_BASE], WX_LBD_*)
   wx_i64 n;
   int shift;
   int kind;

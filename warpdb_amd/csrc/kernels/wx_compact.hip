@@ -115,8 +115,24 @@ __device__ __forceinline__ wx_i64 wx_lookback(const WxCompactArgs &a, wx_i64 til
           moved = false;
           spins = 0;
         } else if (now - t_last > WX_STALL_TICKS && spins >= WX_STALL_SPINS) {  // sticky error for the host + this launch's abort word
-          atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_LOOKBACK);
-          wx::st_agent(&a.status[a.n_tiles], abort_word);
+          // report the nearest predecessor still unpublished, and its word
+          int rj = 0, rl = 0;
+          wx_u64 rw = 0ull;
+#pragma unroll
+          for (int j = WX_LB_PER_LANE - 1; j >= 0; --j) {
+            const wx_u64 pm = __builtin_amdgcn_ballot_w64(wx_cflag(st[j], E) == 0ull && 64 * j + lane < near_p);
+            if (pm) {
+              rj = j;
+              rl = __builtin_ctzll(pm);
+              rw = __shfl(st[j], rl);
+            }
+          }
+          if (lane == 0) {
+            wx::lb_report(a.ctrs + WX_LBD_BASE, WX_LBD_COMPACT | ((wx_u64)a.epoch << 8), (wx_u64)tile,
+                          (wx_u64)(look - 64 * rj - rl), rw);
+            atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_LOOKBACK);
+            wx::st_agent(&a.status[a.n_tiles], abort_word);
+          }
         }
         if (wx::ld_agent(&a.status[a.n_tiles]) == abort_word) {
 #pragma unroll

@@ -495,6 +495,12 @@ __device__ __forceinline__ wx_u64 wx_rs_walk(const WxRadixPassArgs &a, wx_u32 ti
       if (t_last == 0ull) {
         t_last = now;
       } else if (now - t_last > WX_STALL_TICKS && spins >= WX_STALL_SPINS) {
+        wx_u64 seen = 0ull;  // the unpublished predecessor p's word
+#pragma unroll
+        for (int j = 0; j < WX_RS_LBW; ++j)
+          if (j == stop) seen = wv[j];
+        wx::lb_report(a.lbd, WX_LBD_RADIX | ((wx_u64)a.epoch << 8) | ((wx_u64)d << 16) | ((wx_u64)(a.shift / 8) << 32),
+                      (wx_u64)tile, (wx_u64)p, seen);
         atomicOr(a.err, WX_DEVERR_LOOKBACK);
         atomicExch(&a.ctl[1], 1u);
       }

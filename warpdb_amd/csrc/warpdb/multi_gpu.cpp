@@ -217,6 +217,15 @@ Comms &comms_for(int ndev) {
 
 namespace {
 
+// Host -> device copy ordered on the shard's stream, where the kernels that
+// read it run (a null-stream hipMemcpy from pageable memory may return before
+// the data lands, and the shard streams are non-blocking); synchronous, so the
+// host buffer may go out of scope.
+void h2d_ordered(void *dst, const void *src, size_t bytes, hipStream_t s) {
+  hip_ok(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, s), "hipMemcpyAsync");
+  hip_ok(hipStreamSynchronize(s), "hipStreamSynchronize");
+}
+
 // ncclAllGather of `bytes` bytes per shard: every shard's `recv` receives
 // all shards' `send` buffers in shard order (co-located virtual shards go
 // through the host; one shard copies unless the one-rank test hook is on).
@@ -237,7 +246,7 @@ void allgather_bytes(const std::vector<ShardRange> &shards, const std::vector<vo
     }
     for (size_t i = 0; i < ns; ++i) {
       DevGuard g(shards[i].device);
-      hip_ok(hipMemcpy(recv[i], all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy");
+      h2d_ordered(recv[i], all.data(), all.size(), streams[i]);
     }
     return;
   }
@@ -271,7 +280,7 @@ void allreduce_f64(const std::vector<ShardRange> &shards, const std::vector<doub
     }
     for (int i = 0; i < nshard; ++i) {
       DevGuard g(shards[i].device);
-      hip_ok(hipMemcpy(bufs[i], acc.data(), count * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+      h2d_ordered(bufs[i], acc.data(), count * sizeof(double), streams[i]);
     }
     return;
   }
@@ -566,7 +575,7 @@ TopkResult ResidentShards::topk_heads(const std::string &order_cuda, const std::
       hip_ok(hipMemcpy(all.data() + rec * i, impl_->topk[i].hrec.ptr, rec, hipMemcpyDeviceToHost), "hipMemcpy");
     }
     DevGuard g(ranges[0].device);
-    hip_ok(hipMemcpy(impl_->topk[0].hall.ptr, all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy");
+    h2d_ordered(impl_->topk[0].hall.ptr, all.data(), all.size(), streams[0]);
   } else if (ns > 1 || exchange_one_rank()) {
     gathered = true;
     impl_->timer.begin(ranges, streams);
@@ -601,6 +610,7 @@ TopkResult ResidentShards::topk_heads(const std::string &order_cuda, const std::
                            &L, static_cast<float *>(t0.hkeys.ptr), static_cast<int64_t *>(t0.hrows.ptr),
                            static_cast<float *>(t0.hvals.ptr), nullptr, &m, err, sizeof(err)),
              err);
+    impl_->timer.end(ranges, streams);  // no-op unless begin ran (a collective), as in topk()
     for (size_t i = 0; i < ns; ++i) {
       DevGuard g(ranges[i].device);
       hip_ok(hipStreamSynchronize(streams[i]), "hipStreamSynchronize");
@@ -663,7 +673,7 @@ TopkResult ResidentShards::topk(const std::string &order_cuda, const std::string
     }
     for (size_t i = 0; i < ns; ++i) {
       DevGuard g(ranges[i].device);
-      hip_ok(hipMemcpy(impl_->topk[i].all.ptr, all.data(), all.size(), hipMemcpyHostToDevice), "hipMemcpy");
+      h2d_ordered(impl_->topk[i].all.ptr, all.data(), all.size(), streams[i]);
     }
   } else if (ns > 1 || exchange_one_rank()) {
     gathered = true;

@@ -145,6 +145,8 @@ def enable_stream_comm(group=None) -> bool:
     something to exchange).  Ranks agree before and after the build, so
     either every rank uses its own communicator or none does (then the
     exchanges stay on torch.distributed, with a warning)."""
+    if not (dist.is_available() and dist.is_initialized()):
+        return False  # no process group: nothing to exchange over
     key = _gkey(group)
     e = _entry(group)
     if e is not None:
