@@ -259,24 +259,62 @@ def line_common(args, world, n_total, elapsed, workload):
 
 
 def roofline(bytes_per_launch, kern_ms, read_bytes, kname, traffic, timing):
+    traffic, traffic_source = traffic
     achieved = bytes_per_launch / (kern_ms * 1e-3) / 1e9
     return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "kernel": kname,
+            "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic, "traffic_source": traffic_source,
+            "kernel": kname,
             "kernel_ms": round(kern_ms, 4), "bytes_per_launch": int(bytes_per_launch), "timing": timing,
             # BASELINE.md's "HBM-read roofline": input bytes only over the same time
             "read_only_frac": round(read_bytes / (kern_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
 
 
+# PMC traffic profiles (profiles/pmc_<workload>.json, written by
+# tools/pmc_record.py after tools/pmc_run.sh): per workload, the dominant
+# kernels with their dispatches per query, and the kernel sources whose text
+# the profile was collected against (wx_args.h + wx_common.hip + the family).
+PMC_FAMILIES = {
+    "project": ({"wx_project_compact_deep": 1}, ["wx_compact.hip"]),
+    "dense": ({"wx_project_dense": 1}, ["wx_dense.hip"]),
+    "sum": ({"wx_reduce_sum": 1}, ["wx_sum.hip"]),
+    "group": ({"wx_group_sum": 1}, ["wx_group.hip"]),
+    "topk": ({"wx_topk_scan": 1}, ["wx_topk.hip"]),
+    "sort": ({"wx_radix_hist_": 1, "wx_radix_tile_": 4}, ["wx_radix.hip"]),
+    "group_wide": ({"wx_group_part_": None}, ["wx_group_part.hip"]),  # every dispatch of the pipeline, once
+}
+
+
+def kernel_src_sha16(workload):
+    import hashlib
+
+    h = hashlib.sha256()
+    kdir = os.path.join(ROOT, "warpdb_amd", "csrc", "kernels")
+    for name in ["wx_args.h", "wx_common.hip"] + PMC_FAMILIES[workload][1]:
+        with open(os.path.join(kdir, name), "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
 def pmc_traffic(workload, n, keys=1024):
+    """(HBM bytes per launch scaled to n rows, provenance).  The bytes are
+    null when the profile is missing or was collected against other kernel
+    sources than the ones in the tree (stale): re-run tools/pmc_run.sh."""
     if workload == "group" and keys > 2048:  # the many-key (partitioned) pipeline has its own passes
         workload = "group_wide"
-    pmc = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
-    if os.path.exists(pmc):
-        with open(pmc) as f:
-            d = json.load(f)
-        if d.get("rows"):
-            return round(d["hbm_bytes_per_launch"] * n / d["rows"])
-    return None
+    rel = f"profiles/pmc_{workload}.json"
+    pmc = os.path.join(ROOT, rel)
+    if not os.path.exists(pmc) or workload not in PMC_FAMILIES:
+        return None, {"file": None}
+    with open(pmc) as f:
+        d = json.load(f)
+    src = {"file": rel, "collected": d.get("collected"), "kernel_src_sha16": d.get("kernel_src_sha16"),
+           "rows": d.get("rows")}
+    cur = kernel_src_sha16(workload)
+    src["current"] = d.get("kernel_src_sha16") == cur
+    if not src["current"] or not d.get("rows"):
+        src["stale_reason"] = f"kernel sources changed since collection (tree {cur})"
+        return None, src
+    return round(d["hbm_bytes_per_launch"] * n / d["rows"]), src
 
 
 # ------------------------------------------------- result check

@@ -10,7 +10,9 @@
 #   prof:NAME[:BENCH ARGS]     the same bench under rocprofv3 --kernel-trace --stats
 #                              (NAME_kernel_stats.csv is the summary to keep)
 #   pmc:NAME[:BENCH ARGS]      FETCH_SIZE and WRITE_SIZE passes (one counter block
-#                              each) over 3 steps, summarised to NAME_pmc.json
+#                              each) over 3 steps, summarised to NAME_pmc.json and
+#                              recorded in profiles/pmc_<workload>.json (copied
+#                              under gpurun_out/TAG/: copy it back into profiles/)
 #   py:NAME:SCRIPT [ARGS]      python3 SCRIPT ARGS > NAME.txt
 #   pyprof:NAME:SCRIPT [ARGS]  the same under rocprofv3 --kernel-trace --stats
 set -euo pipefail
@@ -57,7 +59,14 @@ for STEP in "$@"; do
           python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-secondary $ARGS \
           > "$O/pmc_$NAME/$C.log" 2>&1)
       done
-      python3 tools/pmc_summary.py $(find "$O/pmc_$NAME" -name "*counter_collection.csv") > "$O/${NAME}_pmc.json" ;;
+      python3 tools/pmc_summary.py $(find "$O/pmc_$NAME" -name "*counter_collection.csv") > "$O/${NAME}_pmc.json"
+      # the tracked profiles/pmc_<workload>.json bench.py reads (date + kernel-source sha)
+      PW=$(echo " $ARGS " | sed -n 's/.* --workload \([a-z_]*\) .*/\1/p')
+      PW=${PW:-project}
+      [[ "$PW" == group && "$ARGS" == *--keys* ]] && PW=group_wide
+      PR=$(echo " $ARGS " | sed -n 's/.* --rows \([0-9.e]*\) .*/\1/p')
+      python3 tools/pmc_record.py "$PW" "${PR:-1e9}" "$O/${NAME}_pmc.json" "gpu_run.sh $TAG/$NAME"
+      cp "profiles/pmc_$PW.json" "$O/" ;;
     pyprof)
       # the script under rocprofv3 --kernel-trace --stats (NAME_kernel_stats.csv, prof_NAME/)
       SCRIPT=${ARGS%% *}

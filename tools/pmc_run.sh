@@ -17,3 +17,8 @@ for C in FETCH_SIZE WRITE_SIZE; do
 done
 python3 "$R/tools/pmc_summary.py" $(find "$OUT" -name "*counter_collection.csv") > "$OUT/summary.json"
 cat "$OUT/summary.json"
+# the tracked record bench.py reads (collection date + kernel-source sha)
+PW=$W
+[[ "$W" == group && "$EXTRA" == *--keys* ]] && PW=group_wide
+python3 "$R/tools/pmc_record.py" "$PW" "$ROWS" "$OUT/summary.json" "$TAG"
+cp "$R/profiles/pmc_$PW.json" "$OUT/"

@@ -22,7 +22,9 @@
 #endif
 // K up to this keeps the fully unrolled insertion (C5's K = 5); larger K
 // takes the rolled one (compile time, below)
+#ifndef WX_TOPK_UNROLLED_MAX
 #define WX_TOPK_UNROLLED_MAX 8
+#endif
 // K from this up keeps 8-row lane lists and a spill list per wave (below):
 // 1.95 vs 2.20 ms per 1e9 rows at K = 32, but 1.01 vs 0.80 at K = 9 and
 // 1.17 vs 0.98 at K = 16, where the K-row lane lists' own filter still pays
@@ -162,7 +164,7 @@ __device__ __forceinline__ void block_merge(TopListT<C> &L, wx_u32 (*s_k)[WX_TOP
 // inserts.  A row is dropped only when K better rows are held (a full spill
 // list) or when it is worse than the bound T, so the lanes' lists and the
 // spill list together hold the wave's top K.
-#define WX_TOPK_LANE WX_TOPK_UNROLLED_MAX
+#define WX_TOPK_LANE 8
 struct SpillList {
   wx_u32 k = 0u;              // entry `lane` (lanes >= K hold nothing)
   wx_i64 i = WX_IDX_NONE;
