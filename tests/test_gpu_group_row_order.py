@@ -146,3 +146,61 @@ def test_row_order_general_path_keys_with_nan_bit_patterns():
     assert g == len(rk) == len(special)
     assert np.array_equal(k, rk) and np.array_equal(c, rc)
     assert np.array_equal(bits(s), bits(rs))
+
+
+def _adversarial_groups(rng, n):
+    """Per-group value streams that push the exact block-parallel fold
+    (wx::fold_exact) onto every branch: round-half-even ties against a large
+    running sum, sums that cancel through zero and hover at a power of two,
+    binade crossings both ways, negative sums, NaN / Inf, denormal floats,
+    overflow, and plain prices (the fast path)."""
+    g = rng.integers(0, 10, n).astype(np.int32)
+    v = np.empty(n, np.float32)
+    for key in range(10):
+        m = int((g == key).sum())
+        if key == 0:    # ties: 2^30 first, then odd / even multiples of 2^-23 (half of u = 2^-22)
+            x = rng.integers(-8, 9, m).astype(np.float32) * np.float32(2.0 ** -23)
+            x[0] = 2.0 ** 30
+        elif key == 1:  # cancellation through zero
+            x = np.where(rng.random(m) < 0.5, 1e7, -1e7).astype(np.float32) + rng.uniform(-1, 1, m).astype(np.float32)
+        elif key == 2:  # prices
+            x = rng.uniform(0.0, 40.0, m).astype(np.float32)
+        elif key == 3:  # a NaN midway
+            x = rng.uniform(0.0, 40.0, m).astype(np.float32)
+            x[m // 2] = np.float32("nan")
+        elif key == 4:  # +inf, then -inf: NaN
+            x = rng.uniform(0.0, 1.0, m).astype(np.float32)
+            x[m // 3] = np.float32("inf")
+            x[2 * m // 3] = np.float32("-inf")
+        elif key == 5:  # denormals and tiny values under a large sum
+            x = (rng.integers(1, 1 << 20, m).astype(np.float32) * np.float32(2.0 ** -149)).astype(np.float32)
+            x[::97] = np.float32(3.0e6)
+        elif key == 6:  # hovering at 2^20: +-x steps across the power of two
+            x = (rng.choice(np.array([1.0, -1.0], np.float32), m) * rng.uniform(0.0, 3.0, m)).astype(np.float32)
+            x[0] = 2.0 ** 20
+        elif key == 7:  # negative sums crossing binades
+            x = -rng.uniform(0.0, 1000.0, m).astype(np.float32)
+        elif key == 8:  # float-max values: a double sum far above the float range
+            x = np.full(m, 3.0e38, np.float32)
+        else:           # mixed scales (the spread_values mix), negative too
+            x = spread_values(rng, m) * rng.choice(np.array([1.0, -1.0], np.float32), m)
+        v[g == key] = x
+    return v, g
+
+
+@pytest.mark.parametrize("path", ["span", "general"])
+def test_row_order_exact_fold_adversarial(path):
+    n = 400_003
+    rng = np.random.default_rng(41)
+    v, g = _adversarial_groups(rng, n)
+    keys = g if path == "span" else g * 1000  # a key span > 2048 takes the general path
+    cols = {"price": v, "quantity": keys.astype(np.int32)}
+    got_g, k, s, c = run(cols, None, 64)
+    assert got_g == 10 and np.array_equal(k, np.unique(keys))
+    for i, key in enumerate(np.unique(keys)):
+        want = np.add.accumulate(v[keys == key].astype(np.float64))[-1]  # the sequential fold, row order
+        assert c[i] == int((keys == key).sum())
+        if np.isnan(want):
+            assert np.isnan(s[i]), (key, s[i])
+        else:
+            assert bits(s[i]) == bits(want), (key, s[i], want)

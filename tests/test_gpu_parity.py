@@ -582,15 +582,15 @@ def test_topk_seed_pass(k, data, monkeypatch):
 
 
 def test_topk_seed_pass_default_size():
-    # the default seed rule (K > 8 over tables of 2^24 rows and more), ties at
-    # the winners
+    # the default seed rule (K >= 5 over tables of 2^24 rows and more; K = 4
+    # runs without it), ties at the winners
     n = (1 << 24) + 5
     p = (np.round(synth.uniform_f32(n, 34, 0.0, 40.0) * 4.0) / 4.0).astype(np.float32)
     cols = {"price": p}
     table, _ = dev_table(cols)
     keys = torch.empty(32, device="cuda")
     idx = torch.empty(32, dtype=torch.int64, device="cuda")
-    for k, desc in ((9, True), (32, False)):
+    for k, desc in ((4, True), (5, True), (5, False), (9, True), (32, False)):
         m = wx.topk(table, "price[idx]", None, None, k, desc, launch(), keys.data_ptr(), idx.data_ptr())
         rk, ri, _ = ora.topk(ora.HostTable(cols), "price", k, desc)
         assert m == len(rk) == k

@@ -13,7 +13,11 @@ for w in "project:--rows 2e7 --c4-rows 80000001 --c3-rows 40000001" "sum:--total
   name=${w%%:*}; args=${w#*:}
   case $name in group_keys) wl="";; *) wl="--workload $name";; esac
   P=$((P + 1))
+  t0=$(date +%s.%N)
   WARPDB_DIST_BACKEND=gloo timeout -k 10 300 python3 -m torch.distributed.run --nnodes=1 --nproc-per-node "$N" \
     --master-addr 127.0.0.1 --master-port $P bench.py --gpus "$N" $wl --steps 3 --warmup 1 $args \
     > "$O/${name}_${N}rank.json" 2> "$O/${name}_${N}rank.err" || { echo "$name failed"; exit 1; }
+  t1=$(date +%s.%N)
+  # wall time of the whole launch (torchrun start, N imports, data, warm-up, timed steps, checks)
+  echo "$name ${N} ranks: $(awk "BEGIN{printf \"%.1f\", $t1 - $t0}") s wall" | tee -a "$O/wall_${N}rank.txt"
 done

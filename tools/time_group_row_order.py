@@ -6,7 +6,9 @@ key-span path (counting scatter + fold, keys spanning <= 2048) and the
 general path (compactions + radix pair sort + fold, WARPDB_GROUP_ROWS=general);
 their sums must agree bit for bit.
 
-usage: python tools/time_group_row_order.py [rows] [keys] [reps]
+usage: python tools/time_group_row_order.py [rows] [keys] [reps] [variant;variant;...]
+(variants: WARPDB_EXTRA_DEFINES lists for the row-order runs, e.g.
+";WX_FOLD_EXACT=0" -- every variant's sums must equal the first's bit for bit)
 """
 import os
 import sys
@@ -30,9 +32,15 @@ wx.fill_synthetic(key.data_ptr(), wx.INT32, n, 3, 1, 0, nk - 1, L0)
 table = wx.Table.from_tensors(price=price, quantity=key)
 cap = max(4096, 2 * nk)
 out = {}
-for label, flags in (("plain", wx.F_SYNC), ("row-order", wx.F_ROW_ORDER | wx.F_SYNC),
-                     ("row-order general", wx.F_ROW_ORDER | wx.F_SYNC)):
-    if label == "row-order general":
+variants = sys.argv[4].split(";") if len(sys.argv) > 4 else [os.environ.get("WARPDB_EXTRA_DEFINES", "")]
+runs = [("plain", wx.F_SYNC, "")]
+for var in variants:
+    tag = f" [{var}]" if var else ""
+    runs += [("row-order" + tag, wx.F_ROW_ORDER | wx.F_SYNC, var),
+             ("row-order general" + tag, wx.F_ROW_ORDER | wx.F_SYNC, var)]
+for label, flags, var in runs:
+    os.environ["WARPDB_EXTRA_DEFINES"] = var
+    if label.startswith("row-order general"):
         os.environ["WARPDB_GROUP_ROWS"] = "general"
     ok = torch.empty(cap, dtype=torch.int32, device="cuda")
     os_ = torch.empty(cap, dtype=torch.float64, device="cuda")
@@ -51,13 +59,16 @@ for label, flags in (("plain", wx.F_SYNC), ("row-order", wx.F_ROW_ORDER | wx.F_S
     ts.sort()
     out[label] = (ok[:g].clone(), os_[:g].clone(), oc[:g].clone())
     os.environ.pop("WARPDB_GROUP_ROWS", None)
-    print(f"{label:17s} {n} rows x {nk} keys: median {ts[len(ts) // 2] * 1e3:.2f} ms, min {ts[0] * 1e3:.2f} ms "
+    print(f"{label:40s} {n} rows x {nk} keys: median {ts[len(ts) // 2] * 1e3:.2f} ms, min {ts[0] * 1e3:.2f} ms "
           f"({g} groups)", flush=True)
-(k0, s0, c0), (k1, s1, c1) = out["plain"], out["row-order"]
-(k2, s2, c2) = out["row-order general"]
-assert torch.equal(k1, k2) and torch.equal(c1, c2)
-assert torch.equal(s1.view(torch.int64), s2.view(torch.int64)), "the two row-order paths differ"
-print("row-order key-span path == general path, bit for bit")
+(k0, s0, c0) = out["plain"]
+first = [lab for lab, _, _ in runs if lab != "plain"]
+(k1, s1, c1) = out[first[0]]
+for lab in first[1:]:
+    (k2, s2, c2) = out[lab]
+    assert torch.equal(k1, k2) and torch.equal(c1, c2)
+    assert torch.equal(s1.view(torch.int64), s2.view(torch.int64)), f"{lab} differs from {first[0]}"
+print(f"row-order sums equal bit for bit across {len(first)} runs (key-span and general paths, every variant)")
 assert torch.equal(k0, k1) and torch.equal(c0, c1)
 rel = ((s1 - s0).abs() / s1.abs().clamp_min(1e-300)).max().item()
 diff = int((s1.view(torch.int64) != s0.view(torch.int64)).sum().item())

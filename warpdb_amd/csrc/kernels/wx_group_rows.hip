@@ -403,6 +403,9 @@ extern "C" __global__ __launch_bounds__(1024) void wx_ro_base(WxRoBaseArgs a) {
 extern "C" __global__ __launch_bounds__(64) void wx_ro_fold(WxRoFoldArgs a) {
   constexpr int U = WX_RO_FOLD_AHEAD;
   __shared__ double s_fold[2][64];
+#if WX_FOLD_EXACT
+  __shared__ double s_xf[WX_XF_B];
+#endif
   const int lane = threadIdx.x;
   for (wx_i64 g = blockIdx.x; g < a.n_groups; g += gridDim.x) {
     wx_i64 start = 0;
@@ -411,6 +414,12 @@ extern "C" __global__ __launch_bounds__(64) void wx_ro_fold(WxRoFoldArgs a) {
     for (int o = 32; o >= 1; o >>= 1) start += __shfl_xor(start, o);
     const wx_i64 c = a.gcounts[g];
     const float *v = a.svals + start;
+#if WX_FOLD_EXACT
+    const double xs = wx::fold_exact(v, c, s_xf);
+    if (lane == 0) a.out_sums[g] = xs;
+    __builtin_amdgcn_wave_barrier();
+    continue;
+#endif
     const wx_i64 nch = (c + 63) >> 6;
     double s = 0.0;
     // chunk 0 staged in half 0; chunks 1 .. U in flight (xr[u] = chunk u + 1)

@@ -585,6 +585,110 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// The row-order fold s = (((s + v0) + v1) + ...) in double, bit for bit, WITHOUT
+// one dependent add per value.  While the running sum s stays inside one binade
+// [2^k, 2^(k+1)), every double it can take is a multiple of u = 2^(k-52), so
+// each step is fl(s + v) = s + round_u(v): a multiple of u plus v rounded to
+// the nearest multiple of u (ties to even excepted -- then the parity of s
+// decides).  So a block of 64 * WX_XF_J values whose steps provably stay in
+// the binade folds to s + u * sum(round_u(v_i)), an exact integer sum, in any
+// order: q_i = v_i * 2^(52 - k) (exact), r_i = rint(q_i); the block takes the
+// fast path when no q_i is a tie (fraction exactly 1/2) or large (|q_i| < 2^44,
+// so every sum of 512 of them is an exact double), and every state S + prefix
+// stays strictly inside (2^52, 2^53) in magnitude -- checked conservatively
+// against S +- sum(|r_i|).  Any other block (s = 0 at the start, a binade
+// crossing, a tie, NaN / Inf, tiny s) runs the dependent adds in row order
+// through an LDS broadcast.  Prices U[0, 40) at ~1e6 rows per group: ~12 of
+// ~2 000 blocks per group take the slow path (the first, and one per doubling).
+#ifndef WX_FOLD_EXACT
+#define WX_FOLD_EXACT 1  // the row-order folds use fold_exact; 0: one dependent add per value (A/B)
+#endif
+#ifndef WX_XF_J
+#define WX_XF_J 8  // values per lane per block (block = 64 * WX_XF_J)
+#endif
+#ifndef WX_XF_AHEAD
+#define WX_XF_AHEAD 8  // blocks whose loads are in flight ahead of the fold
+#endif
+#define WX_XF_B (64 * WX_XF_J)
+static_assert(WX_XF_B <= 512, "sums of |q| < 2^44 stay exact doubles for at most 512 values");
+
+namespace wx {
+// one block, value (j, lane) at row j * 64 + lane of the block; every lane
+// returns the same s; lds: 64 * WX_XF_J doubles of this wave
+__device__ __forceinline__ double xf_block(double s, const float (&x)[WX_XF_J], double *lds) {
+  const double as = __builtin_fabs(s);
+  if (as >= 0x1p-900 && as < 0x1p1000) {  // wave-uniform; 0, tiny, huge, NaN, Inf: the slow path
+    const int k = __builtin_amdgcn_frexp_exp(s) - 1;  // |s| in [2^k, 2^(k+1))
+    bool ok = true;
+    double t = 0.0, a = 0.0;
+#pragma unroll
+    for (int j = 0; j < WX_XF_J; ++j) {
+      const double q = __builtin_ldexp((double)x[j], 52 - k);  // exact (an underflow is far below a tie)
+      const double r = __builtin_rint(q);
+      ok = ok && __builtin_fabs(q) < 0x1p44 && q - __builtin_floor(q) != 0.5;  // false for NaN / Inf
+      t += r;  // integers below 2^53 in every partial sum: exact
+      a += __builtin_fabs(r);
+    }
+    if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) {
+      t = wave_sum_f64(t);
+      a = wave_sum_f64(a);
+      const double S = __builtin_ldexp(s, 52 - k);  // the integer s / u, |S| in [2^52, 2^53)
+      const bool fits = s > 0.0 ? (S - a > 0x1p52 && S + a < 0x1p53) : (S + a < -0x1p52 && S - a > -0x1p53);
+      if (fits) return __builtin_ldexp(S + t, k - 52);
+    }
+  }
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int j = 0; j < WX_XF_J; ++j) lds[j * 64 + lane] = (double)x[j];
+  __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): one wave, LDS in order
+  __builtin_amdgcn_wave_barrier();
+  for (int i = 0; i < WX_XF_B; i += 16) {
+    double d[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) d[q] = lds[i + q];
+#pragma unroll
+    for (int q = 0; q < 16; ++q) s += d[q];
+  }
+  __builtin_amdgcn_wave_barrier();  // every lane's reads done before the next block's writes
+  return s;
+}
+
+// s = ((0 + v[0]) + v[1]) + ... + v[c - 1] in double, bit for bit; one wave.
+// A block past the end is padded with +0.0, which leaves any running sum
+// unchanged (it starts at +0.0, so it is never -0.0).
+__device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *lds) {
+  const int lane = threadIdx.x & 63;
+  constexpr int D = WX_XF_AHEAD;
+  const wx_i64 nb = (c + WX_XF_B - 1) / WX_XF_B;
+  float xr[D][WX_XF_J];
+#pragma unroll
+  for (int d = 0; d < D; ++d)
+#pragma unroll
+    for (int j = 0; j < WX_XF_J; ++j) {
+      const wx_i64 i = (wx_i64)d * WX_XF_B + j * 64 + lane;
+      xr[d][j] = i < c ? v[i] : 0.0f;
+    }
+  double s = 0.0;
+  for (wx_i64 b0 = 0; b0 < nb; b0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const wx_i64 b = b0 + d;
+      if (b >= nb) break;  // wave-uniform
+      float x[WX_XF_J];
+#pragma unroll
+      for (int j = 0; j < WX_XF_J; ++j) {
+        x[j] = xr[d][j];
+        const wx_i64 i = (b + D) * WX_XF_B + j * 64 + lane;
+        xr[d][j] = i < c ? v[i] : 0.0f;
+      }
+      s = xf_block(s, x, lds);
+    }
+  }
+  return s;
+}
+}  // namespace wx
+
 // Row-order GROUP BY sums (WX_F_ROW_ORDER, warpexec.cpp do_group_sum_rows):
 // one wave per group.  The wave finds the group's first row in the
 // key-sorted array (lower bound), checks that exactly its count of rows
@@ -625,6 +729,15 @@ extern "C" __global__ __launch_bounds__(64) void wx_group_fold(WxGroupFoldArgs a
       continue;
     }
     const float *v = a.svals + lo;
+#if WX_FOLD_EXACT
+    {
+      __shared__ double s_xf[WX_XF_B];
+      const double xs = wx::fold_exact(v, c, s_xf);
+      if (lane == 0) a.out_sums[g] = xs;
+      __builtin_amdgcn_wave_barrier();
+      continue;
+    }
+#endif
     double s = 0.0;
     for (wx_i64 base = 0; base < c; base += 64 * WX_FOLD_U) {
       wx_u32 x[WX_FOLD_U];
