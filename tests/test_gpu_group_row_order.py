@@ -204,3 +204,26 @@ def test_row_order_exact_fold_adversarial(path):
             assert np.isnan(s[i]), (key, s[i])
         else:
             assert bits(s[i]) == bits(want), (key, s[i], want)
+
+
+@pytest.mark.parametrize("outlier", [None, 1000, 5000, -3000])
+def test_row_order_direct_span_guess(outlier, monkeypatch):
+    """The span path without the ordinary call: the 2048-key span is guessed
+    from a strided sample (or the memo), so a key the sample misses either
+    still falls inside the centred span (1000) or makes the count kernel flag
+    the miss and the call fall back to the ordinary call first (5000, -3000:
+    then the general path, the keys spanning > 2048).  Equal, bit for bit, to
+    the oracle and to the ordinary-call-first span path."""
+    n = 500_003
+    rng = np.random.default_rng(47)
+    q = rng.integers(0, 100, n).astype(np.int32)
+    if outlier is not None:
+        q[n // 2 + 1] = outlier  # one row: a 65 536-row strided sample misses it
+    cols = {"price": spread_values(rng, n), "quantity": q}
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", capacity=4096)
+    for mode in ("span", "ordinary"):
+        monkeypatch.setenv("WARPDB_GROUP_ROWS", mode)
+        for _ in range(2):  # the second call takes the memo's range
+            g, k, s, c = run(cols, None, 4096)
+            assert g == len(rk) and np.array_equal(k, rk) and np.array_equal(c, rc), mode
+            assert np.array_equal(bits(s), bits(rs)), mode

@@ -205,17 +205,24 @@ def test_hip_many_key_group_by_equals_reference(path, monkeypatch):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("path", ["window", "window+hash", "hash", "partitioned"])
-def test_hip_row_order_group_by_equals_reference(path, monkeypatch):
+@pytest.mark.parametrize("path,rows", [("window", "span")] + [(p, r) for r in ("ordinary", "general")
+                                                                for p in ("window", "window+hash", "hash", "partitioned")])
+def test_hip_row_order_group_by_equals_reference(path, rows, monkeypatch):
     """WX_F_ROW_ORDER against the reference's own row-order fold on a table
-    where the order shows in the bits (workload_c3o.npz): the LDS window
-    (key_lo 0), half the keys in the general-key hash (key_lo 100), all of
-    them there (key_lo 10^6), and the range-partitioned first step (forced
-    by the WARPDB_GP_MIN_ROWS test hook)."""
+    where the order shows in the bits (workload_c3o.npz), by every row-order
+    route (WARPDB_GROUP_ROWS): the key-span path straight from the table
+    ("span", the default), the key-span path after the ordinary call
+    ("ordinary") and the general compaction + radix-sort path ("general");
+    the ordinary call itself by the LDS window (key_lo 0), half the keys in
+    the general-key hash (key_lo 100), all of them there (key_lo 10^6), and
+    the range-partitioned first step (forced by the WARPDB_GP_MIN_ROWS test
+    hook)."""
     torch = pytest.importorskip("torch")
     from test_gpu_parity import dev_table
     from warpdb_amd import _warpexec as wx
 
+    # (the direct key-span path makes no ordinary call: key_lo and the ordinary paths do not apply to it)
+    monkeypatch.setenv("WARPDB_GROUP_ROWS", rows)
     key_lo = {"window": 0, "window+hash": 100, "hash": 1_000_000, "partitioned": 0}[path]
     if path == "partitioned":
         monkeypatch.setenv("WARPDB_GP_MIN_ROWS", "0")

@@ -13,6 +13,8 @@
 #                              each) over 3 steps, summarised to NAME_pmc.json and
 #                              recorded in profiles/pmc_<workload>.json (copied
 #                              under gpurun_out/TAG/: copy it back into profiles/)
+#   sq:NAME[:BENCH ARGS]       SQ wave-cycle accounting (WAIT_ANY / WAIT_INST_ANY /
+#                              ACTIVE_INST_ANY / LDS counters) in one pass, NAME_sq.json
 #   py:NAME:SCRIPT [ARGS]      python3 SCRIPT ARGS > NAME.txt
 #   pyprof:NAME:SCRIPT [ARGS]  the same under rocprofv3 --kernel-trace --stats
 set -euo pipefail
@@ -67,6 +69,18 @@ for STEP in "$@"; do
       PR=$(echo " $ARGS " | sed -n 's/.* --rows \([0-9.e]*\) .*/\1/p')
       python3 tools/pmc_record.py "$PW" "${PR:-1e9}" "$O/${NAME}_pmc.json" "gpu_run.sh $TAG/$NAME"
       cp "profiles/pmc_$PW.json" "$O/" ;;
+    sq)
+      # wave-cycle accounting of the bench's kernels in one pass (8 SQ slots + 1 GRBM):
+      # WAIT_ANY (parked: s_waitcnt / barrier) + WAIT_INST_ANY (issue stall) +
+      # ACTIVE_INST_ANY ~= WAVE_CYCLES; summarised per kernel to NAME_sq.json
+      mkdir -p "$O/sq_$NAME"
+      # shellcheck disable=SC2086
+      (cd /tmp && timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+        SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_INSTS_VALU SQ_INSTS_LDS GRBM_GUI_ACTIVE \
+        -d "$O/sq_$NAME" -o run --output-format csv -- \
+        python3 "$R/bench.py" --steps 3 --warmup 1 --no-cpu-baseline --no-check --no-secondary $ARGS \
+        > "$O/sq_$NAME/run.log" 2>&1)
+      python3 tools/pmc_summary.py $(find "$O/sq_$NAME" -name "*counter_collection.csv") > "$O/${NAME}_sq.json" ;;
     pyprof)
       # the script under rocprofv3 --kernel-trace --stats (NAME_kernel_stats.csv, prof_NAME/)
       SCRIPT=${ARGS%% *}

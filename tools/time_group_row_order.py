@@ -2,7 +2,8 @@
 """Wall time of GROUP BY with and without WX_F_ROW_ORDER on bench.py's C3
 table (price f32 U[0, 40), quantity int32 U{0..keys-1}), per call, and the
 row-order sums' distance from the ordinary ones.  Row order runs twice: the
-key-span path (counting scatter + fold, keys spanning <= 2048) and the
+key-span path (counting scatter + fold, keys spanning <= 2048; straight
+from the table, then after an ordinary call, WARPDB_GROUP_ROWS=ordinary) and the
 general path (compactions + radix pair sort + fold, WARPDB_GROUP_ROWS=general);
 their sums must agree bit for bit.
 
@@ -37,11 +38,14 @@ runs = [("plain", wx.F_SYNC, "")]
 for var in variants:
     tag = f" [{var}]" if var else ""
     runs += [("row-order" + tag, wx.F_ROW_ORDER | wx.F_SYNC, var),
+             ("row-order ordinary-first" + tag, wx.F_ROW_ORDER | wx.F_SYNC, var),
              ("row-order general" + tag, wx.F_ROW_ORDER | wx.F_SYNC, var)]
 for label, flags, var in runs:
     os.environ["WARPDB_EXTRA_DEFINES"] = var
     if label.startswith("row-order general"):
         os.environ["WARPDB_GROUP_ROWS"] = "general"
+    elif label.startswith("row-order ordinary-first"):
+        os.environ["WARPDB_GROUP_ROWS"] = "ordinary"  # the span path after an ordinary call
     ok = torch.empty(cap, dtype=torch.int32, device="cuda")
     os_ = torch.empty(cap, dtype=torch.float64, device="cuda")
     oc = torch.empty(cap, dtype=torch.int64, device="cuda")

@@ -423,6 +423,7 @@ struct WxRoArgs {
   const wx_u32 *off;  // wx_ro_scatter: [ranges][2048] first output slot of each bin in each range
   float *out;         // wx_ro_scatter: the passing rows' values, key-major, row order within a key
   wx_u64 *ctrs;       // [1]: error bits (a key outside the span)
+  wx_i64 *info;       // nullable; the direct path: [2] set when a key lies outside the span (no error bit)
 };
 
 struct WxRoScanArgs {
@@ -440,7 +441,16 @@ struct WxRoBaseArgs {
   const wx_i64 *gcounts;   // [n_groups]
   wx_i64 n_groups;
   int key_lo;
-  wx_u64 *ctrs;            // [1]: error bits (counts that do not match)
+  wx_u64 *ctrs;            // [1]: error bits (counts that do not match; capacity)
+  // the direct path (out_counts set): the groups come from the totals instead
+  // of an ordinary call -- keys / counts of the non-empty bins in ascending
+  // order (at most capacity of them), their number, and info[0] groups,
+  // info[1] passing rows, info[3] / info[4] the smallest / largest key
+  int *out_keys;
+  wx_i64 *out_counts;
+  wx_i64 capacity;
+  wx_i64 *n_groups_out;
+  wx_i64 *info;
 };
 
 struct WxRoFoldArgs {

@@ -97,7 +97,12 @@ extern "C" __global__ __launch_bounds__(WX_RO_BLOCK) void wx_ro_count(WxRoArgs w
   wx_i64 b = e0;
   for (; b + SPAN <= e1; b += SPAN) wx_ro_count_span<true>(wx_a, h, b, e1, copy, bad);
   if (b < e1) wx_ro_count_span<false>(wx_a, h, b, e1, copy, bad);
-  if (bad) atomicOr(reinterpret_cast<unsigned int *>(&wx_a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+  if (bad) {
+    if (wx_a.info)  // the direct path's guessed span missed a key: the host falls back
+      atomicOr(reinterpret_cast<unsigned int *>(&wx_a.info[2]), 1u);
+    else
+      atomicOr(reinterpret_cast<unsigned int *>(&wx_a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+  }
   __syncthreads();
   for (int i = threadIdx.x; i < WX_RO_BINS; i += WX_RO_BLOCK) {
     wx_u32 c = 0u;
@@ -124,38 +129,29 @@ struct WxRoShared {
 #define WX_RO_LOAD(name, T, slot) \
   wx_n##slot[i] = (WHOLE || e < wx_a.n_rows) ? static_cast<const T *>(wx_a.col[slot])[e] : static_cast<T>(0);
 #define WX_RO_BIND(name, T, slot) const ::wx::reg<T> name{wx_n##slot[i]};
+// unconditional load at a clamped row (the pipelined loop: no branch between the loads)
+#define WX_RO_LOADC(name, T, slot) \
+  wx_n##slot[i] = static_cast<const T *>(wx_a.col[slot])[e < wx_a.n_rows ? e : wx_a.n_rows - 1];
+#define WX_RO_PARAM(name, T, slot) , const T (&wx_n##slot)[WX_RO_ITEMS]
+#define WX_RO_ARG(name, T, slot) , wx_n##slot
 
 // Tile t of range r (run[]: the range's next output slot of this thread's
 // bins BPT * tid + j).  Row i * 64 + lane of wave w's 1024 rows is row
 // t * TILE + w * 1024 + i * 64 + lane, so (wave, item, lane) is row order.
 // Two 512-thread workgroups per CU hide each other's loads.
-template <bool WHOLE>
-__device__ __forceinline__ void wx_ro_tile(const WxRoArgs &wx_a, WxRoShared &S, float *s_v, wx_i64 t,
-                                           wx_u32 (&run)[WX_RO_BPT], bool &bad) {
-  typedef wx_u32 u4 __attribute__((ext_vector_type(4)));
-  // an opaque copy of the thread index: the slot and address arithmetic is
-  // formed here, not hoisted out of the tile loop into spilled registers
-  int tid = threadIdx.x;
-  asm volatile("" : "+v"(tid));
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wp = wave >> 1, sh = (wave & 1) * 16;
-  const wx_u64 below = (1ull << lane) - 1ull;
-  wx_u32 *wcf = &S.wc[0][0];
-  const wx_i64 wb = t * WX_RO_TILE + wave * 64 * WX_RO_ITEMS + lane;
-  // (0) the tile's rows: bin (0xffffffff = not passing) and value; whole
-  // tiles load every row unconditionally (all loads in flight together)
-  wx_u32 bin[WX_RO_ITEMS];
-  float val[WX_RO_ITEMS];
-  WX_COLS(WX_RO_DECL)
-#pragma unroll
-  for (int i = 0; i < WX_RO_ITEMS; ++i) {
-    const wx_i64 e = wb + (wx_i64)i * 64;
-    WX_COLS(WX_RO_LOAD)
+// (0) tile t's rows: bin (0xffffffff = not passing) and value, from the
+// column registers wx_n* (loaded by WX_RO_LOAD_TILE)
+#define WX_RO_LOAD_TILE(t_, LOADX)                                                                \
+  {                                                                                               \
+    const wx_i64 wb_ = (t_) * WX_RO_TILE + (threadIdx.x >> 6) * 64 * WX_RO_ITEMS + (threadIdx.x & 63); \
+    _Pragma("unroll") for (int i = 0; i < WX_RO_ITEMS; ++i) {                                    \
+      const wx_i64 e = wb_ + (wx_i64)i * 64;                                                      \
+      WX_COLS(LOADX)                                                                               \
+    }                                                                                             \
   }
-  // every load issued before any row is evaluated (the scheduler would
-  // otherwise wait for each row's loads in turn to save registers)
-  __builtin_amdgcn_sched_barrier(0);
+template <bool WHOLE>
+__device__ __forceinline__ void wx_ro_eval(const WxRoArgs &wx_a, wx_i64 wb, wx_u32 (&bin)[WX_RO_ITEMS],
+                                           float (&val)[WX_RO_ITEMS], bool &bad WX_COLS(WX_RO_PARAM)) {
 #pragma unroll
   for (int i = 0; i < WX_RO_ITEMS; ++i) {
     const wx_i64 idx = wb + (wx_i64)i * 64;
@@ -171,6 +167,42 @@ __device__ __forceinline__ void wx_ro_tile(const WxRoArgs &wx_a, WxRoShared &S, 
       }
     }
   }
+}
+
+// Steps (1)-(4) of tile t from its rows' bins and values.
+__device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S, float *s_v,
+                                            wx_u32 (&run)[WX_RO_BPT], wx_u32 (&bin)[WX_RO_ITEMS],
+                                            const float (&val)[WX_RO_ITEMS]);
+
+template <bool WHOLE>
+__device__ __forceinline__ void wx_ro_tile(const WxRoArgs &wx_a, WxRoShared &S, float *s_v, wx_i64 t,
+                                           wx_u32 (&run)[WX_RO_BPT], bool &bad) {
+  const wx_i64 wb = t * WX_RO_TILE + (threadIdx.x >> 6) * 64 * WX_RO_ITEMS + (threadIdx.x & 63);
+  // whole tiles load every row unconditionally (all loads in flight together)
+  wx_u32 bin[WX_RO_ITEMS];
+  float val[WX_RO_ITEMS];
+  WX_COLS(WX_RO_DECL)
+  WX_RO_LOAD_TILE(t, WX_RO_LOAD)
+  // every load issued before any row is evaluated (the scheduler would
+  // otherwise wait for each row's loads in turn to save registers)
+  __builtin_amdgcn_sched_barrier(0);
+  wx_ro_eval<WHOLE>(wx_a, wb, bin, val, bad WX_COLS(WX_RO_ARG));
+  wx_ro_place(wx_a, S, s_v, run, bin, val);
+}
+
+__device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S, float *s_v,
+                                            wx_u32 (&run)[WX_RO_BPT], wx_u32 (&bin)[WX_RO_ITEMS],
+                                            const float (&val)[WX_RO_ITEMS]) {
+  typedef wx_u32 u4 __attribute__((ext_vector_type(4)));
+  // an opaque copy of the thread index: the slot and address arithmetic is
+  // formed here, not hoisted out of the tile loop into spilled registers
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wp = wave >> 1, sh = (wave & 1) * 16;
+  const wx_u64 below = (1ull << lane) - 1ull;
+  wx_u32 *wcf = &S.wc[0][0];
   // (1) stable in-wave ranks: one returning LDS add per passing row on the
   // wave's counter (the LDS returns same-address lanes' results in ascending
   // lane order, gfx950); lane 0's bin group adds its size once from lane 0
@@ -282,7 +314,13 @@ __device__ __forceinline__ void wx_ro_tile(const WxRoArgs &wx_a, WxRoShared &S, 
   __syncthreads();  // counters zeroed
 }
 
-extern "C" __global__ __launch_bounds__(WX_RO_BLOCK, 2 * WX_RO_BLOCK / 256) void wx_ro_scatter(WxRoArgs wx_a) {
+#ifndef WX_RO_PIPE
+#define WX_RO_PIPE 0  // 1: tile t + 1's column loads in flight while tile t is ranked and stored
+#endif
+#ifndef WX_RO_WGPC
+#define WX_RO_WGPC 2  // scatter workgroups per CU (the host reads the same define)
+#endif
+extern "C" __global__ __launch_bounds__(WX_RO_BLOCK, WX_RO_WGPC * WX_RO_BLOCK / 256) void wx_ro_scatter(WxRoArgs wx_a) {
   typedef wx_u32 u4 __attribute__((ext_vector_type(4)));
   __shared__ WxRoShared S;
   __shared__ float s_v[WX_RO_TILE];
@@ -298,17 +336,39 @@ extern "C" __global__ __launch_bounds__(WX_RO_BLOCK, 2 * WX_RO_BLOCK / 256) void
   __syncthreads();  // counters zeroed
   bool bad = false;
   const wx_i64 n_whole = wx_a.n_rows / WX_RO_TILE;  // tiles [0, n_whole) are whole
+#if WX_RO_PIPE
+  // software-pipelined: tile t's rows evaluated out of the column registers,
+  // tile t + 1's loads issued into them, then tile t ranked, permuted, stored
+  WX_COLS(WX_RO_DECL)
+  WX_RO_LOAD_TILE(t0, WX_RO_LOADC)
+  for (wx_i64 t = t0; t < t1; ++t) {
+    wx_u32 bin[WX_RO_ITEMS];
+    float val[WX_RO_ITEMS];
+    const wx_i64 wb = t * WX_RO_TILE + (threadIdx.x >> 6) * 64 * WX_RO_ITEMS + (threadIdx.x & 63);
+    if (t < n_whole)
+      wx_ro_eval<true>(wx_a, wb, bin, val, bad WX_COLS(WX_RO_ARG));
+    else
+      wx_ro_eval<false>(wx_a, wb, bin, val, bad WX_COLS(WX_RO_ARG));
+    if (t + 1 < t1) WX_RO_LOAD_TILE(t + 1, WX_RO_LOADC)
+    wx_ro_place(wx_a, S, s_v, run, bin, val);
+  }
+#else
   for (wx_i64 t = t0; t < t1; ++t) {
     if (t < n_whole)
       wx_ro_tile<true>(wx_a, S, s_v, t, run, bad);
     else
       wx_ro_tile<false>(wx_a, S, s_v, t, run, bad);
   }
+#endif
   if (bad) atomicOr(reinterpret_cast<unsigned int *>(&wx_a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
 }
 #undef WX_RO_DECL
 #undef WX_RO_LOAD
 #undef WX_RO_BIND
+#undef WX_RO_PARAM
+#undef WX_RO_ARG
+#undef WX_RO_LOAD_TILE
+#undef WX_RO_LOADC
 #endif  // WX_OP == WX_OP_GROUP
 
 #if WX_OP == WX_OP_UTIL
@@ -370,6 +430,51 @@ extern "C" __global__ __launch_bounds__(1024) void wx_ro_base(WxRoBaseArgs a) {
   b.x = lb;
   b.y = lb + t2.x;
   *reinterpret_cast<u2 *>(a.base + 2 * tid) = b;
+  if (a.out_counts) {
+    // the direct path: groups = the non-empty bins, in key order
+    const wx_u32 nz = (t2.x ? 1u : 0u) + (t2.y ? 1u : 0u);
+    const wx_u32 ginc = wx_ro_wave_incl(nz);
+    __shared__ wx_u32 gs[16];
+    __shared__ int s_kmin, s_kmax;
+    if (lane == 63) gs[wave] = ginc;
+    if (tid == 0) {
+      s_kmin = 0x7fffffff;
+      s_kmax = (int)0x80000000;
+    }
+    __syncthreads();
+    wx_u32 gi = ginc - nz, ng = 0u;
+    for (int w = 0; w < 16; ++w) {
+      gi += w < wave ? gs[w] : 0u;
+      ng += gs[w];
+    }
+    if (t2.x) {
+      if (gi < a.capacity) {
+        a.out_keys[gi] = a.key_lo + 2 * tid;
+        a.out_counts[gi] = t2.x;
+      }
+      atomicMin(&s_kmin, a.key_lo + 2 * tid);
+      atomicMax(&s_kmax, a.key_lo + 2 * tid);
+      ++gi;
+    }
+    if (t2.y) {
+      if (gi < a.capacity) {
+        a.out_keys[gi] = a.key_lo + 2 * tid + 1;
+        a.out_counts[gi] = t2.y;
+      }
+      atomicMin(&s_kmin, a.key_lo + 2 * tid + 1);
+      atomicMax(&s_kmax, a.key_lo + 2 * tid + 1);
+    }
+    __syncthreads();
+    if (tid == 0) {
+      if (a.n_groups_out) *a.n_groups_out = ng;
+      a.info[0] = ng;
+      a.info[1] = all;
+      a.info[3] = s_kmin;
+      a.info[4] = s_kmax;
+      if ((wx_i64)ng > a.capacity) atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_CAPACITY);
+    }
+    return;
+  }
   bool bad = false;
   wx_i64 sum = 0;
   for (wx_i64 g = tid; g < a.n_groups; g += 1024) {

@@ -608,31 +608,49 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
 #define WX_XF_J 8  // values per lane per block (block = 64 * WX_XF_J)
 #endif
 #ifndef WX_XF_AHEAD
-#define WX_XF_AHEAD 8  // blocks whose loads are in flight ahead of the fold
+#define WX_XF_AHEAD 4  // blocks whose loads are in flight ahead of the fold (8: 512 VGPRs + scratch)
 #endif
 #define WX_XF_B (64 * WX_XF_J)
 static_assert(WX_XF_B <= 512, "sums of |q| < 2^44 stay exact doubles for at most 512 values");
 
 namespace wx {
+// Wave total of a double, every lane the same value: an inclusive DPP scan
+// (row shifts, then row broadcasts; no LDS round trips, unlike __shfl_xor's
+// ds_bpermute) and lane 63's result read back.  Exact for the fold's
+// integer-valued sums (< 2^53), so the add order does not matter.
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const wx_u64 u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(wx_u32)u, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(wx_u32)(u >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __longlong_as_double((long long)(((wx_u64)(wx_u32)hi << 32) | (wx_u32)lo));
+}
+__device__ __forceinline__ double wave_total_f64(double v) {
+  v += dpp_f64<0x111, 0xf>(v);  // row_shr:1
+  v += dpp_f64<0x112, 0xf>(v);  // row_shr:2
+  v += dpp_f64<0x114, 0xf>(v);  // row_shr:4
+  v += dpp_f64<0x118, 0xf>(v);  // row_shr:8
+  v += dpp_f64<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f64<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+  const wx_u64 u = __double_as_longlong(v);
+  const wx_u32 lo = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)u, 63);
+  const wx_u32 hi = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)(u >> 32), 63);
+  return __longlong_as_double((long long)(((wx_u64)hi << 32) | lo));
+}
+
 // one block, value (j, lane) at row j * 64 + lane of the block; every lane
 // returns the same s; lds: 64 * WX_XF_J doubles of this wave
+__device__ __forceinline__ void xf_sums(int k, const float (&x)[WX_XF_J], double &t, double &a, bool &ok);
 __device__ __forceinline__ double xf_block(double s, const float (&x)[WX_XF_J], double *lds) {
   const double as = __builtin_fabs(s);
   if (as >= 0x1p-900 && as < 0x1p1000) {  // wave-uniform; 0, tiny, huge, NaN, Inf: the slow path
     const int k = __builtin_amdgcn_frexp_exp(s) - 1;  // |s| in [2^k, 2^(k+1))
-    bool ok = true;
-    double t = 0.0, a = 0.0;
-#pragma unroll
-    for (int j = 0; j < WX_XF_J; ++j) {
-      const double q = __builtin_ldexp((double)x[j], 52 - k);  // exact (an underflow is far below a tie)
-      const double r = __builtin_rint(q);
-      ok = ok && __builtin_fabs(q) < 0x1p44 && q - __builtin_floor(q) != 0.5;  // false for NaN / Inf
-      t += r;  // integers below 2^53 in every partial sum: exact
-      a += __builtin_fabs(r);
-    }
-    if (__builtin_amdgcn_ballot_w64(!ok) == 0ull) {
-      t = wave_sum_f64(t);
-      a = wave_sum_f64(a);
+    double t, a;
+    bool ok;
+    xf_sums(k, x, t, a, ok);
+    if (ok) {
+      t = wave_total_f64(t);
+      a = wave_total_f64(a);
       const double S = __builtin_ldexp(s, 52 - k);  // the integer s / u, |S| in [2^52, 2^53)
       const bool fits = s > 0.0 ? (S - a > 0x1p52 && S + a < 0x1p53) : (S + a < -0x1p52 && S - a > -0x1p53);
       if (fits) return __builtin_ldexp(S + t, k - 52);
@@ -654,10 +672,46 @@ __device__ __forceinline__ double xf_block(double s, const float (&x)[WX_XF_J], 
   return s;
 }
 
+// v[i] for i < c, else +0.0 (padding), without a branch: the load always
+// issues, at a clamped index (c >= 1)
+__device__ __forceinline__ float xf_load(const float *v, wx_i64 i, wx_i64 c) {
+  const float x = v[i < c ? i : c - 1];
+  return i < c ? x : 0.0f;
+}
+
+// The block sums of a block under binade k: t = sum r_i, a = sum |r_i| (lane
+// partials), ok = no tie / large / non-finite q anywhere in the block.  q =
+// x * 2^(52 - k) is exact (a power-of-two scaling; an underflow is far below
+// a tie, an overflow fails |q| < 2^44); r = rint(q) by the 1.5 * 2^52 add
+// and subtract (round half to even, exact for |q| < 2^51); a tie is |q - r|
+// = 1/2 exactly.  Full-rate adds and multiplies only.
+__device__ __forceinline__ void xf_sums(int k, const float (&x)[WX_XF_J], double &t, double &a, bool &ok) {
+  const double p2 = __builtin_ldexp(1.0, 52 - k);
+  constexpr double M = 0x1.8p52;
+  bool lok = true;
+  t = 0.0;
+  a = 0.0;
+#pragma unroll
+  for (int j = 0; j < WX_XF_J; ++j) {
+    const double q = (double)x[j] * p2;
+    const double r = (q + M) - M;
+    lok = lok && __builtin_fabs(q) < 0x1p44 && __builtin_fabs(q - r) != 0.5;  // false for NaN / Inf
+    t += r;
+    a += __builtin_fabs(r);
+  }
+  ok = __builtin_amdgcn_ballot_w64(!lok) == 0ull;
+}
+
 // s = ((0 + v[0]) + v[1]) + ... + v[c - 1] in double, bit for bit; one wave.
+// Blocks go WX_XF_AHEAD at a time: their sums are formed together under the
+// binade of the running sum at the group's start (independent reductions the
+// scheduler interleaves, off the chain), then applied in order, each after
+// checking that the running sum is still in that binade and the block fits;
+// a block that does not is folded by xf_block from the exact running sum.
 // A block past the end is padded with +0.0, which leaves any running sum
 // unchanged (it starts at +0.0, so it is never -0.0).
 __device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *lds) {
+  if (c <= 0) return 0.0;
   const int lane = threadIdx.x & 63;
   constexpr int D = WX_XF_AHEAD;
   const wx_i64 nb = (c + WX_XF_B - 1) / WX_XF_B;
@@ -667,22 +721,47 @@ __device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *l
 #pragma unroll
     for (int j = 0; j < WX_XF_J; ++j) {
       const wx_i64 i = (wx_i64)d * WX_XF_B + j * 64 + lane;
-      xr[d][j] = i < c ? v[i] : 0.0f;
+      xr[d][j] = xf_load(v, i, c);
     }
   double s = 0.0;
   for (wx_i64 b0 = 0; b0 < nb; b0 += D) {
+    // this group's values out of the ring, the next group's loads out
+    float xc[D][WX_XF_J];
 #pragma unroll
-    for (int d = 0; d < D; ++d) {
-      const wx_i64 b = b0 + d;
-      if (b >= nb) break;  // wave-uniform
-      float x[WX_XF_J];
+    for (int d = 0; d < D; ++d)
 #pragma unroll
       for (int j = 0; j < WX_XF_J; ++j) {
-        x[j] = xr[d][j];
-        const wx_i64 i = (b + D) * WX_XF_B + j * 64 + lane;
-        xr[d][j] = i < c ? v[i] : 0.0f;
+        xc[d][j] = xr[d][j];
+        const wx_i64 i = (b0 + D + d) * WX_XF_B + j * 64 + lane;
+        xr[d][j] = xf_load(v, i, c);
       }
-      s = xf_block(s, x, lds);
+    const double as0 = __builtin_fabs(s);
+    const bool sok = as0 >= 0x1p-900 && as0 < 0x1p1000;  // wave-uniform
+    const int k = sok ? __builtin_amdgcn_frexp_exp(s) - 1 : 0;
+    double t[D], a[D];
+    bool ok[D];
+#pragma unroll
+    for (int d = 0; d < D; ++d) xf_sums(k, xc[d], t[d], a[d], ok[d]);
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      t[d] = wave_total_f64(t[d]);
+      a[d] = wave_total_f64(a[d]);
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      if (b0 + d >= nb) break;  // wave-uniform
+      const double as = __builtin_fabs(s);
+      bool done = false;
+      if (sok && ok[d] && as >= 0x1p-900 && __builtin_amdgcn_frexp_exp(s) - 1 == k) {
+        const double S = __builtin_ldexp(s, 52 - k);
+        const bool fits =
+            s > 0.0 ? (S - a[d] > 0x1p52 && S + a[d] < 0x1p53) : (S + a[d] < -0x1p52 && S - a[d] > -0x1p53);
+        if (fits) {
+          s = __builtin_ldexp(S + t[d], k - 52);
+          done = true;
+        }
+      }
+      if (!done) s = xf_block(s, xc[d], lds);
     }
   }
   return s;
