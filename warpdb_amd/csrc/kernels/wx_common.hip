@@ -172,7 +172,7 @@ __device__ __forceinline__ void st_agent(wx_u64 *p, wx_u64 v) {
 
 // Look-back abort report (wx_args.h WX_LBD_*): the first aborting waiter of
 // a workspace claims the record and fills it; one lane calls this.
-__device__ __noinline__ void lb_report(wx_u64 *lbd, wx_u64 what, wx_u64 tile, wx_u64 pred, wx_u64 word) {
+__device__ __forceinline__ void lb_report(wx_u64 *lbd, wx_u64 what, wx_u64 tile, wx_u64 pred, wx_u64 word) {
   if (atomicCAS(&lbd[0], 0ull, 1ull) != 0ull) return;
   st_agent(&lbd[1], what);
   st_agent(&lbd[2], tile);

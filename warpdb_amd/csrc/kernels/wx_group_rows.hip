@@ -129,9 +129,6 @@ struct WxRoShared {
 #define WX_RO_LOAD(name, T, slot) \
   wx_n##slot[i] = (WHOLE || e < wx_a.n_rows) ? static_cast<const T *>(wx_a.col[slot])[e] : static_cast<T>(0);
 #define WX_RO_BIND(name, T, slot) const ::wx::reg<T> name{wx_n##slot[i]};
-// unconditional load at a clamped row (the pipelined loop: no branch between the loads)
-#define WX_RO_LOADC(name, T, slot) \
-  wx_n##slot[i] = static_cast<const T *>(wx_a.col[slot])[e < wx_a.n_rows ? e : wx_a.n_rows - 1];
 #define WX_RO_PARAM(name, T, slot) , const T (&wx_n##slot)[WX_RO_ITEMS]
 #define WX_RO_ARG(name, T, slot) , wx_n##slot
 
@@ -314,13 +311,11 @@ __device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S,
   __syncthreads();  // counters zeroed
 }
 
-#ifndef WX_RO_PIPE
-#define WX_RO_PIPE 0  // 1: tile t + 1's column loads in flight while tile t is ranked and stored
-#endif
-#ifndef WX_RO_WGPC
-#define WX_RO_WGPC 2  // scatter workgroups per CU (the host reads the same define)
-#endif
-extern "C" __global__ __launch_bounds__(WX_RO_BLOCK, WX_RO_WGPC * WX_RO_BLOCK / 256) void wx_ro_scatter(WxRoArgs wx_a) {
+// (Measured and dropped, round 6, profiles/r06/group_row_order_ab.txt: tile
+// t + 1's column loads in flight while tile t is ranked and stored -- 52 B of
+// scratch at two workgroups per CU (18.2 ms per query), 158 VGPRs at one
+// (7.61 vs 7.38 ms).)
+extern "C" __global__ __launch_bounds__(WX_RO_BLOCK, 2 * WX_RO_BLOCK / 256) void wx_ro_scatter(WxRoArgs wx_a) {
   typedef wx_u32 u4 __attribute__((ext_vector_type(4)));
   __shared__ WxRoShared S;
   __shared__ float s_v[WX_RO_TILE];
@@ -336,30 +331,12 @@ extern "C" __global__ __launch_bounds__(WX_RO_BLOCK, WX_RO_WGPC * WX_RO_BLOCK / 
   __syncthreads();  // counters zeroed
   bool bad = false;
   const wx_i64 n_whole = wx_a.n_rows / WX_RO_TILE;  // tiles [0, n_whole) are whole
-#if WX_RO_PIPE
-  // software-pipelined: tile t's rows evaluated out of the column registers,
-  // tile t + 1's loads issued into them, then tile t ranked, permuted, stored
-  WX_COLS(WX_RO_DECL)
-  WX_RO_LOAD_TILE(t0, WX_RO_LOADC)
-  for (wx_i64 t = t0; t < t1; ++t) {
-    wx_u32 bin[WX_RO_ITEMS];
-    float val[WX_RO_ITEMS];
-    const wx_i64 wb = t * WX_RO_TILE + (threadIdx.x >> 6) * 64 * WX_RO_ITEMS + (threadIdx.x & 63);
-    if (t < n_whole)
-      wx_ro_eval<true>(wx_a, wb, bin, val, bad WX_COLS(WX_RO_ARG));
-    else
-      wx_ro_eval<false>(wx_a, wb, bin, val, bad WX_COLS(WX_RO_ARG));
-    if (t + 1 < t1) WX_RO_LOAD_TILE(t + 1, WX_RO_LOADC)
-    wx_ro_place(wx_a, S, s_v, run, bin, val);
-  }
-#else
   for (wx_i64 t = t0; t < t1; ++t) {
     if (t < n_whole)
       wx_ro_tile<true>(wx_a, S, s_v, t, run, bad);
     else
       wx_ro_tile<false>(wx_a, S, s_v, t, run, bad);
   }
-#endif
   if (bad) atomicOr(reinterpret_cast<unsigned int *>(&wx_a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
 }
 #undef WX_RO_DECL
@@ -368,7 +345,6 @@ extern "C" __global__ __launch_bounds__(WX_RO_BLOCK, WX_RO_WGPC * WX_RO_BLOCK / 
 #undef WX_RO_PARAM
 #undef WX_RO_ARG
 #undef WX_RO_LOAD_TILE
-#undef WX_RO_LOADC
 #endif  // WX_OP == WX_OP_GROUP
 
 #if WX_OP == WX_OP_UTIL
