@@ -227,3 +227,38 @@ def test_row_order_direct_span_guess(outlier, monkeypatch):
             g, k, s, c = run(cols, None, 4096)
             assert g == len(rk) and np.array_equal(k, rk) and np.array_equal(c, rc), mode
             assert np.array_equal(bits(s), bits(rs)), mode
+
+
+@pytest.mark.parametrize("path", ["span", "general"])
+@pytest.mark.parametrize("values", ["prices", "spread", "ties"])
+def test_row_order_big_group_chunked(path, values):
+    """A group of more than WX_XF_BIG (4 Mi) rows is folded in 64 Ki-value
+    chunks (wx_xf_big_*: approximate chunk sums, exact chunk sums under a
+    guessed binade, applied in order after checking it, fold_exact for the
+    rest) instead of one wave streaming it alone; the sums stay bit-equal
+    to the sequential fold, with prices (chunks mostly applied whole), with
+    mixed 1e7 / 1 / 1e-3 scales (chunks mostly refolded), and with half the
+    values ties against a 2^33 running sum (the tie scan of every block and
+    chunk)."""
+    n = 10_000_003
+    rng = np.random.default_rng(53)
+    q = np.where(rng.random(n) < 0.85, 7, rng.integers(0, 1000, n)).astype(np.int32)
+    if path == "general":
+        q = q * 1000  # a key span > 2048
+    if values == "prices":
+        v = rng.uniform(0.0, 40.0, n).astype(np.float32)
+    elif values == "spread":
+        v = spread_values(rng, n)
+    else:  # half of the values ties against the running sum: multiples of 2^-20 under a 1.5 * 2^33 sum (u = 2^-19)
+        v = (rng.integers(-8, 9, n).astype(np.float32) * np.float32(2.0 ** -20)).astype(np.float32)
+        v[np.flatnonzero(q == (7000 if path == "general" else 7))[0]] = np.float32(1.5 * 2.0 ** 33)  # mid-binade
+    cols = {"price": v, "quantity": q}
+    g, k, s, c = run(cols, None, 4096)
+    uk = np.unique(q)
+    assert g == len(uk) and np.array_equal(k, uk)
+    big = int(np.argmax(c))
+    assert c[big] > 4 * (1 << 20)
+    for i in (big, 0, g - 1):
+        want = np.add.accumulate(v[q == k[i]].astype(np.float64))[-1]
+        assert c[i] == int((q == k[i]).sum())
+        assert bits(s[i]) == bits(want), (i, s[i], want)

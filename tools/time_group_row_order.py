@@ -9,7 +9,8 @@ their sums must agree bit for bit.
 
 usage: python tools/time_group_row_order.py [rows] [keys] [reps] [variant;variant;...]
 (variants: WARPDB_EXTRA_DEFINES lists for the row-order runs, e.g.
-";WX_FOLD_EXACT=0" -- every variant's sums must equal the first's bit for bit)
+";WX_FOLD_EXACT=0" -- every variant's sums must equal the first's bit for bit;
+ROW_SKEW=0.9 puts 90 % of the rows on one key)
 """
 import os
 import sys
@@ -30,6 +31,9 @@ price = torch.empty(n, dtype=torch.float32, device="cuda")
 key = torch.empty(n, dtype=torch.int32, device="cuda")
 wx.fill_synthetic(price.data_ptr(), wx.FLOAT32, n, 1, 0, 0.0, 40.0, L0)
 wx.fill_synthetic(key.data_ptr(), wx.INT32, n, 3, 1, 0, nk - 1, L0)
+skew = float(os.environ.get("ROW_SKEW", "0"))  # this share of the rows on key 7 (a big group)
+if skew > 0:
+    key.masked_fill_(torch.rand(n, device="cuda") < skew, 7)
 table = wx.Table.from_tensors(price=price, quantity=key)
 cap = max(4096, 2 * nk)
 out = {}

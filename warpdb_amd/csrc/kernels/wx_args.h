@@ -358,6 +358,21 @@ struct WxGroupFoldArgs {
   wx_i64 n_groups;
   double *out_sums;        // [n_groups]
   wx_u64 *ctrs;            // [1]: error bits (a group whose rows do not match its count)
+  wx_i64 skip_above;       // > 0: groups of more rows are folded by the wx_xf_big_* kernels instead
+};
+
+// Row-order folds of groups larger than WX_XF_BIG rows, split into chunks of
+// WX_XF_CHUNK values (wx_xf_big_approx / _exact / _combine, wx_util.hip).
+#define WX_XF_CHUNK (1 << 16)
+#define WX_XF_BIG (4 << 20)
+struct WxXfBigArgs {
+  const float *svals;   // key-major values, row order within a group
+  const wx_i64 *ent;    // [n_ent][4]: group index, first value, values, first chunk (ascending)
+  int n_ent;
+  wx_i64 n_chunks;      // chunks over all entries
+  double *approx;       // [n_chunks] each chunk's sum in any order
+  double *rec;          // [n_chunks][8] under a guessed binade: k, sum r (ties after the first), bound on sum |r|, ok, has a tie, cf
+  double *out_sums;     // [n_groups]
 };
 
 struct WxSortPrepArgs {
@@ -458,6 +473,7 @@ struct WxRoFoldArgs {
   const wx_i64 *gcounts;   // [n_groups]
   wx_i64 n_groups;
   double *out_sums;        // [n_groups]
+  wx_i64 skip_above;       // > 0: groups of more rows are folded by the wx_xf_big_* kernels instead
 };
 
 struct WxSumFinArgs {

@@ -495,6 +495,7 @@ extern "C" __global__ __launch_bounds__(64) void wx_ro_fold(WxRoFoldArgs a) {
     for (int o = 32; o >= 1; o >>= 1) start += __shfl_xor(start, o);
     const wx_i64 c = a.gcounts[g];
     const float *v = a.svals + start;
+    if (a.skip_above > 0 && c > a.skip_above) continue;  // folded by the wx_xf_big_* kernels
 #if WX_FOLD_EXACT
     const double xs = wx::fold_exact(v, c, s_xf);
     if (lane == 0) a.out_sums[g] = xs;

@@ -594,13 +594,17 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
 // decides).  So a block of 64 * WX_XF_J values whose steps provably stay in
 // the binade folds to s + u * sum(round_u(v_i)), an exact integer sum, in any
 // order: q_i = v_i * 2^(52 - k) (exact), r_i = rint(q_i); the block takes the
-// fast path when no q_i is a tie (fraction exactly 1/2) or large (|q_i| < 2^44,
-// so every sum of 512 of them is an exact double), and every state S + prefix
-// stays strictly inside (2^52, 2^53) in magnitude -- checked conservatively
-// against S +- sum(|r_i|).  Any other block (s = 0 at the start, a binade
-// crossing, a tie, NaN / Inf, tiny s) runs the dependent adds in row order
-// through an LDS broadcast.  Prices U[0, 40) at ~1e6 rows per group: ~12 of
-// ~2 000 blocks per group take the slow path (the first, and one per doubling).
+// fast path when no q_i is large (|q_i| < 2^44, so every sum of 512 of them is
+// an exact double) or non-finite, and every state S + prefix stays strictly
+// inside (2^52, 2^53) in magnitude -- checked conservatively against S +-
+// sum(|r_i|).  A tie (q_i = m + 1/2) rounds to the even one of S + m and S + m
+// + 1, so it depends on the parity of the running integer S and leaves S even:
+// XfTies scans the block in row order by ballots and reduces every tie after
+// the first to a known +0 / +1, and the first to p_in ^ cf (p_in: S's parity
+// where the block starts).  Any other block (s = 0 at the start, a binade
+// crossing, NaN / Inf, tiny s) runs the dependent adds in row order through an
+// LDS broadcast.  Prices U[0, 40) at ~1e6 rows per group: ~12 of ~2 000 blocks
+// per group take the slow path (the first, and one per doubling).
 #ifndef WX_FOLD_EXACT
 #define WX_FOLD_EXACT 1  // the row-order folds use fold_exact; 0: one dependent add per value (A/B)
 #endif
@@ -638,22 +642,126 @@ __device__ __forceinline__ double wave_total_f64(double v) {
   return __longlong_as_double((long long)(((wx_u64)hi << 32) | lo));
 }
 
+// The ties of a row-ordered run of values, 64 at a time (lane l = the l-th
+// value of a row), wave-uniform.  b is rint(q), or floor(q) for a tie; a tie
+// adds b + ((P + b) & 1) where P is the parity of S before it, and leaves S
+// even, so P is known for every tie after the first (the parity of the b's
+// since the tie before it), and the first one's +1 is p_in ^ cf.
+struct XfTies {
+  wx_u32 seen = 0u;  // a tie earlier in this run
+  wx_u32 cpar = 0u;  // parity of the b's since the last tie (since the start, relative to p_in, if none)
+  wx_u32 has = 0u;   // the run has a tie: its first adds p_in ^ cf
+  wx_u32 cf = 0u;
+  double adj = 0.0;  // the +1s of the other ties
+  __device__ __forceinline__ void row(bool tie, bool bpar) {
+    const wx_u64 pm = __builtin_amdgcn_ballot_w64(bpar), tm = __builtin_amdgcn_ballot_w64(tie);
+    if (tm == 0ull) {
+      cpar ^= (wx_u32)__builtin_popcountll(pm) & 1u;
+      return;
+    }
+    const int lane = threadIdx.x & 63;
+    const wx_u64 below = (1ull << lane) - 1ull;
+    bool plus = false;
+    wx_u32 cf_l = 0u;
+    if (tie) {
+      const wx_u64 tb = tm & below;
+      const wx_u32 bp = bpar ? 1u : 0u;
+      if (tb) {  // the tie before it is in this row: the b's strictly between them
+        const int lt = 63 - __builtin_clzll(tb);
+        plus = ((((wx_u32)__builtin_popcountll(pm & below & ~((2ull << lt) - 1ull))) & 1u) ^ bp) != 0u;
+      } else if (seen) {  // in an earlier row
+        plus = ((cpar ^ ((wx_u32)__builtin_popcountll(pm & below) & 1u)) ^ bp) != 0u;
+      } else {  // the run's first tie
+        cf_l = (cpar ^ ((wx_u32)__builtin_popcountll(pm & below) & 1u)) ^ bp;
+      }
+    }
+    adj += (double)__builtin_popcountll(__builtin_amdgcn_ballot_w64(plus));
+    if (!seen) {
+      has = 1u;
+      cf = (wx_u32)__builtin_amdgcn_readlane((int)cf_l, __builtin_ctzll(tm));
+    }
+    const int lt = 63 - __builtin_clzll(tm);
+    cpar = (wx_u32)__builtin_popcountll(pm & ~((2ull << lt) - 1ull)) & 1u;
+    seen = 1u;
+  }
+  // the first tie's +1 (0 without a tie) once S, the running integer where
+  // the run starts, is known (the rest, t + adj, is formed off the chain)
+  __device__ __forceinline__ double first(double S) const {
+    if (!has) return 0.0;  // wave-uniform
+    const double h = S * 0.5;
+    return (double)((h != __builtin_floor(h) ? 1u : 0u) ^ cf);
+  }
+};
+
+// one value under the scaling p2: its b and tie flag (r = rint(q) by the
+// 1.5 * 2^52 add and subtract, round half to even, exact for |q| < 2^51)
+__device__ __forceinline__ double xf_b(double q, bool &tie) {
+  constexpr double M = 0x1.8p52;
+  const double r = (q + M) - M;
+  tie = __builtin_fabs(q - r) == 0.5;
+  return tie && r > q ? r - 1.0 : r;  // a tie's lower neighbour m = floor(q)
+}
+__device__ __forceinline__ bool xf_odd(double b) {
+  const double h = b * 0.5;
+  return h != __builtin_floor(h);
+}
+
+// The sums of a block under binade k: t = sum b_i, a = sum |b_i| + ties (a
+// bound on sum |r_i|) as lane partials, ok = no large / non-finite q, T = the
+// block's ties (rows j = 0 .. WX_XF_J - 1, value (j, lane) at row j * 64 +
+// lane).  q = x * 2^(52 - k) is exact (a power-of-two scaling; an underflow
+// is far below a tie, an overflow fails |q| < 2^44).
+__device__ __forceinline__ void xf_sums(int k, const float (&x)[WX_XF_J], double &t, double &a, bool &ok,
+                                        XfTies &T) {
+  const double p2 = __builtin_ldexp(1.0, 52 - k);
+  constexpr double M = 0x1.8p52;
+  bool lok = true, any = false;
+  t = 0.0;
+  a = 0.0;
+#pragma unroll
+  for (int j = 0; j < WX_XF_J; ++j) {
+    const double q = (double)x[j] * p2;
+    const double r = (q + M) - M;  // rint(q), round half to even
+    lok = lok && __builtin_fabs(q) < 0x1p44;  // false for NaN / Inf
+    any = any || __builtin_fabs(q - r) == 0.5;
+    t += r;
+    a += __builtin_fabs(r);
+  }
+  ok = __builtin_amdgcn_ballot_w64(!lok) == 0ull;
+  T = XfTies();
+  if (ok && __builtin_amdgcn_ballot_w64(any) != 0ull) {
+    // rare: the row scan; a tie's b is floor(q), which is rint(q) or one less
+    double dt = 0.0, nt = 0.0;
+#pragma unroll
+    for (int j = 0; j < WX_XF_J; ++j) {
+      const double q = (double)x[j] * p2;
+      bool tie;
+      const double b = xf_b(q, tie);
+      dt += b - ((q + M) - M);
+      nt += tie ? 1.0 : 0.0;
+      T.row(tie, xf_odd(b));
+    }
+    t += dt;
+    a += 2.0 * nt;  // a tie's final step is b or b + 1, and |b| <= |rint(q)| + 1
+  }
+}
+
 // one block, value (j, lane) at row j * 64 + lane of the block; every lane
 // returns the same s; lds: 64 * WX_XF_J doubles of this wave
-__device__ __forceinline__ void xf_sums(int k, const float (&x)[WX_XF_J], double &t, double &a, bool &ok);
 __device__ __forceinline__ double xf_block(double s, const float (&x)[WX_XF_J], double *lds) {
   const double as = __builtin_fabs(s);
   if (as >= 0x1p-900 && as < 0x1p1000) {  // wave-uniform; 0, tiny, huge, NaN, Inf: the slow path
     const int k = __builtin_amdgcn_frexp_exp(s) - 1;  // |s| in [2^k, 2^(k+1))
     double t, a;
     bool ok;
-    xf_sums(k, x, t, a, ok);
+    XfTies T;
+    xf_sums(k, x, t, a, ok, T);
     if (ok) {
       t = wave_total_f64(t);
       a = wave_total_f64(a);
       const double S = __builtin_ldexp(s, 52 - k);  // the integer s / u, |S| in [2^52, 2^53)
       const bool fits = s > 0.0 ? (S - a > 0x1p52 && S + a < 0x1p53) : (S + a < -0x1p52 && S - a > -0x1p53);
-      if (fits) return __builtin_ldexp(S + t, k - 52);
+      if (fits) return __builtin_ldexp(S + (t + T.adj) + T.first(S), k - 52);
     }
   }
   const int lane = threadIdx.x & 63;
@@ -679,30 +787,7 @@ __device__ __forceinline__ float xf_load(const float *v, wx_i64 i, wx_i64 c) {
   return i < c ? x : 0.0f;
 }
 
-// The block sums of a block under binade k: t = sum r_i, a = sum |r_i| (lane
-// partials), ok = no tie / large / non-finite q anywhere in the block.  q =
-// x * 2^(52 - k) is exact (a power-of-two scaling; an underflow is far below
-// a tie, an overflow fails |q| < 2^44); r = rint(q) by the 1.5 * 2^52 add
-// and subtract (round half to even, exact for |q| < 2^51); a tie is |q - r|
-// = 1/2 exactly.  Full-rate adds and multiplies only.
-__device__ __forceinline__ void xf_sums(int k, const float (&x)[WX_XF_J], double &t, double &a, bool &ok) {
-  const double p2 = __builtin_ldexp(1.0, 52 - k);
-  constexpr double M = 0x1.8p52;
-  bool lok = true;
-  t = 0.0;
-  a = 0.0;
-#pragma unroll
-  for (int j = 0; j < WX_XF_J; ++j) {
-    const double q = (double)x[j] * p2;
-    const double r = (q + M) - M;
-    lok = lok && __builtin_fabs(q) < 0x1p44 && __builtin_fabs(q - r) != 0.5;  // false for NaN / Inf
-    t += r;
-    a += __builtin_fabs(r);
-  }
-  ok = __builtin_amdgcn_ballot_w64(!lok) == 0ull;
-}
-
-// s = ((0 + v[0]) + v[1]) + ... + v[c - 1] in double, bit for bit; one wave.
+// s = ((s0 + v[0]) + v[1]) + ... + v[c - 1] in double, bit for bit; one wave.
 // Blocks go WX_XF_AHEAD at a time: their sums are formed together under the
 // binade of the running sum at the group's start (independent reductions the
 // scheduler interleaves, off the chain), then applied in order, each after
@@ -710,8 +795,8 @@ __device__ __forceinline__ void xf_sums(int k, const float (&x)[WX_XF_J], double
 // a block that does not is folded by xf_block from the exact running sum.
 // A block past the end is padded with +0.0, which leaves any running sum
 // unchanged (it starts at +0.0, so it is never -0.0).
-__device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *lds) {
-  if (c <= 0) return 0.0;
+__device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *lds, double s0 = 0.0) {
+  if (c <= 0) return s0;
   const int lane = threadIdx.x & 63;
   constexpr int D = WX_XF_AHEAD;
   const wx_i64 nb = (c + WX_XF_B - 1) / WX_XF_B;
@@ -723,7 +808,7 @@ __device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *l
       const wx_i64 i = (wx_i64)d * WX_XF_B + j * 64 + lane;
       xr[d][j] = xf_load(v, i, c);
     }
-  double s = 0.0;
+  double s = s0;  // +0.0 for a whole group; a running sum is never -0.0 (it starts at +0.0)
   for (wx_i64 b0 = 0; b0 < nb; b0 += D) {
     // this group's values out of the ring, the next group's loads out
     float xc[D][WX_XF_J];
@@ -740,11 +825,12 @@ __device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *l
     const int k = sok ? __builtin_amdgcn_frexp_exp(s) - 1 : 0;
     double t[D], a[D];
     bool ok[D];
+    XfTies T[D];
 #pragma unroll
-    for (int d = 0; d < D; ++d) xf_sums(k, xc[d], t[d], a[d], ok[d]);
+    for (int d = 0; d < D; ++d) xf_sums(k, xc[d], t[d], a[d], ok[d], T[d]);
 #pragma unroll
     for (int d = 0; d < D; ++d) {
-      t[d] = wave_total_f64(t[d]);
+      t[d] = wave_total_f64(t[d]) + T[d].adj;
       a[d] = wave_total_f64(a[d]);
     }
 #pragma unroll
@@ -757,7 +843,7 @@ __device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *l
         const bool fits =
             s > 0.0 ? (S - a[d] > 0x1p52 && S + a[d] < 0x1p53) : (S + a[d] < -0x1p52 && S - a[d] > -0x1p53);
         if (fits) {
-          s = __builtin_ldexp(S + t[d], k - 52);
+          s = __builtin_ldexp(S + t[d] + T[d].first(S), k - 52);
           done = true;
         }
       }
@@ -767,6 +853,162 @@ __device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *l
   return s;
 }
 }  // namespace wx
+
+// ---------------------------------------------------------------------------
+// Groups of more than WX_XF_BIG rows: one wave per group would stream the
+// whole segment alone (≈ 4 GB/s), so the segment is cut into WX_XF_CHUNK-value
+// chunks.  (1) every chunk's sum in any order (an approximation of the
+// running sum where each chunk starts); (2) each chunk but the first forms
+// its exact integer sums under the binade of that approximate start (q = v *
+// 2^(52 - k), |q| < 2^33 so a chunk's sums stay exact doubles; ties by
+// XfTies); (3) one wave per group applies the chunks in order: a chunk whose
+// guessed binade is the exact running sum's and whose states provably stay
+// in it (S -+ sum |r| strictly inside (2^52, 2^53)) adds u * sum r; any
+// other chunk (the first; the binade crossings, ≈ one per doubling of the
+// sum) is folded by fold_exact from the exact running sum.  The result
+// is the dependent chain's, bit for bit.
+__device__ __forceinline__ int wx_xf_entry(const WxXfBigArgs &a, wx_i64 chunk) {
+  int lo = 0, hi = a.n_ent - 1;  // the last entry whose first chunk is <= chunk
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (a.ent[4 * mid + 3] <= chunk) lo = mid;
+    else hi = mid - 1;
+  }
+  return lo;
+}
+
+// A chunk's values stream through a wave 16 loads per lane at a time (a
+// single-wave loop with one load in flight runs at memory latency).
+#define WX_XF_U 16
+extern "C" __global__ __launch_bounds__(64) void wx_xf_big_approx(WxXfBigArgs a) {
+  const int lane = threadIdx.x;
+  for (wx_i64 chunk = blockIdx.x; chunk < a.n_chunks; chunk += gridDim.x) {
+    const int e = wx_xf_entry(a, chunk);
+    const wx_i64 j = chunk - a.ent[4 * e + 3], count = a.ent[4 * e + 2];
+    const wx_i64 b = j * WX_XF_CHUNK, len = count - b < WX_XF_CHUNK ? count - b : WX_XF_CHUNK;
+    const float *v = a.svals + a.ent[4 * e + 1] + b;
+    double acc = 0.0;
+    for (wx_i64 i0 = 0; i0 < len; i0 += 64 * WX_XF_U) {
+      float x[WX_XF_U];
+#pragma unroll
+      for (int u = 0; u < WX_XF_U; ++u) x[u] = wx::xf_load(v, i0 + 64 * u + lane, len);
+#pragma unroll
+      for (int u = 0; u < WX_XF_U; ++u) acc += (double)x[u];
+    }
+    const double t = wx::wave_total_f64(acc);
+    if (lane == 0) a.approx[chunk] = t;
+  }
+}
+
+extern "C" __global__ __launch_bounds__(64) void wx_xf_big_exact(WxXfBigArgs a) {
+  const int lane = threadIdx.x;
+  for (wx_i64 chunk = blockIdx.x; chunk < a.n_chunks; chunk += gridDim.x) {
+    const int e = wx_xf_entry(a, chunk);
+    const wx_i64 first = a.ent[4 * e + 3], j = chunk - first, count = a.ent[4 * e + 2];
+    if (j == 0) {  // the group's first chunk starts at 0: always folded by the combine
+      if (lane == 0) a.rec[8 * chunk + 3] = 0.0;
+      continue;
+    }
+    double p = 0.0;  // the approximate running sum where this chunk starts
+    for (wx_i64 i = lane; i < j; i += 64) p += a.approx[first + i];
+    p = wx::wave_total_f64(p);
+    const double ap = __builtin_fabs(p);
+    const bool pok = ap >= 0x1p-900 && ap < 0x1p1000;  // wave-uniform; also false for NaN / Inf
+    const int k = pok ? __builtin_amdgcn_frexp_exp(p) - 1 : 0;
+    const double p2 = __builtin_ldexp(1.0, 52 - k);
+    const wx_i64 b = j * WX_XF_CHUNK, len = count - b < WX_XF_CHUNK ? count - b : WX_XF_CHUNK;
+    const float *v = a.svals + a.ent[4 * e + 1] + b;
+    bool lok = pok;
+    double t = 0.0, s_abs = 0.0;
+    wx::XfTies T;  // the chunk's ties in row order (row u of an iteration = values i0 + 64 u ..)
+    for (wx_i64 i0 = 0; i0 < len && pok; i0 += 64 * WX_XF_U) {
+      float x[WX_XF_U];
+#pragma unroll
+      for (int u = 0; u < WX_XF_U; ++u) x[u] = wx::xf_load(v, i0 + 64 * u + lane, len);  // past len: +0.0
+#pragma unroll
+      for (int u = 0; u < WX_XF_U; ++u) {
+        const double q = (double)x[u] * p2;
+        bool tie;
+        const double b = wx::xf_b(q, tie);
+        lok = lok && __builtin_fabs(q) < 0x1p33;
+        t += b;
+        s_abs += __builtin_fabs(b) + (tie ? 1.0 : 0.0);
+        T.row(tie, wx::xf_odd(b));
+      }
+    }
+    const bool ok = __builtin_amdgcn_ballot_w64(!lok) == 0ull;
+    t = wx::wave_total_f64(t);
+    s_abs = wx::wave_total_f64(s_abs);
+    if (lane == 0) {
+      double *r = a.rec + 8 * chunk;
+      r[0] = (double)k;
+      r[1] = t + T.adj;  // + p_in ^ cf when the chunk has a tie (r[4], r[5])
+      r[2] = s_abs;
+      r[3] = ok ? 1.0 : 0.0;
+      r[4] = (double)T.has;
+      r[5] = (double)T.cf;
+    }
+  }
+}
+
+// the chunk records are read 64 at a time (lane l: chunk j0 + l) and taken
+// from the lanes in order, so the walk over a group's chunks waits on memory
+// once per 64 chunks
+__device__ __forceinline__ double wx_xf_lane(double v, int l) {
+  const wx_u64 u = __double_as_longlong(v);
+  const wx_u32 lo = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)u, l);
+  const wx_u32 hi = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)(u >> 32), l);
+  return __longlong_as_double((long long)(((wx_u64)hi << 32) | lo));
+}
+
+extern "C" __global__ __launch_bounds__(64) void wx_xf_big_combine(WxXfBigArgs a) {
+  __shared__ double s_xf[WX_XF_B];
+  const int lane = threadIdx.x;
+  for (int e = blockIdx.x; e < a.n_ent; e += gridDim.x) {
+    const wx_i64 g = a.ent[4 * e], start = a.ent[4 * e + 1], count = a.ent[4 * e + 2], first = a.ent[4 * e + 3];
+    const wx_i64 nch = (count + WX_XF_CHUNK - 1) / WX_XF_CHUNK;
+    double s = 0.0;
+    for (wx_i64 j0 = 0; j0 < nch; j0 += 64) {
+      double rk = 0.0, rt = 0.0, ra = 0.0, rok = 0.0, rhas = 0.0, rcf = 0.0;
+      if (j0 + lane < nch) {
+        const double *r = a.rec + 8 * (first + j0 + lane);
+        rk = r[0];
+        rt = r[1];
+        ra = r[2];
+        rok = r[3];
+        rhas = r[4];
+        rcf = r[5];
+      }
+      const int nl = nch - j0 < 64 ? (int)(nch - j0) : 64;
+      for (int l = 0; l < nl; ++l) {
+        const wx_i64 j = j0 + l;
+        const wx_i64 b = j * WX_XF_CHUNK, len = count - b < WX_XF_CHUNK ? count - b : WX_XF_CHUNK;
+        if (j > 0 && wx_xf_lane(rok, l) != 0.0) {
+          const double as = __builtin_fabs(s);
+          const int k = (int)wx_xf_lane(rk, l);
+          if (as >= 0x1p-900 && as < 0x1p1000 && __builtin_amdgcn_frexp_exp(s) - 1 == k) {
+            const double S = __builtin_ldexp(s, 52 - k), A = wx_xf_lane(ra, l);
+            const bool fits =
+                s > 0.0 ? (S - A > 0x1p52 && S + A < 0x1p53) : (S + A < -0x1p52 && S - A > -0x1p53);
+            if (fits) {
+              double R = wx_xf_lane(rt, l);
+              if (wx_xf_lane(rhas, l) != 0.0) {  // the chunk's first tie: + (S's parity ^ cf)
+                const double h = S * 0.5;
+                const wx_u32 p_in = h != __builtin_floor(h) ? 1u : 0u;
+                R += (double)(p_in ^ (wx_u32)wx_xf_lane(rcf, l));
+              }
+              s = __builtin_ldexp(S + R, k - 52);
+              continue;
+            }
+          }
+        }
+        s = wx::fold_exact(a.svals + start + b, len, s_xf, s);
+      }
+    }
+    if (lane == 0) a.out_sums[g] = s;
+    __builtin_amdgcn_wave_barrier();
+  }
+}
 
 // Row-order GROUP BY sums (WX_F_ROW_ORDER, warpexec.cpp do_group_sum_rows):
 // one wave per group.  The wave finds the group's first row in the
@@ -808,6 +1050,7 @@ extern "C" __global__ __launch_bounds__(64) void wx_group_fold(WxGroupFoldArgs a
       continue;
     }
     const float *v = a.svals + lo;
+    if (a.skip_above > 0 && c > a.skip_above) continue;  // wx_xf_big_* (its count was checked above)
 #if WX_FOLD_EXACT
     {
       __shared__ double s_xf[WX_XF_B];
