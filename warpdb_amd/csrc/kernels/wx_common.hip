@@ -196,6 +196,31 @@ __device__ __forceinline__ double wave_sum_f64(double v) {
   return v;
 }
 
+// Wave total of a double, every lane the same value: an inclusive DPP scan
+// (row shifts, then row broadcasts; no LDS round trips, unlike __shfl_xor's
+// ds_bpermute) and lane 63's result read back.  Every lane must be active.
+// (Exact for the row-order fold's integer-valued sums, < 2^53, so the add
+// order does not matter there.)
+template <int CTRL, int ROW_MASK>
+__device__ __forceinline__ double dpp_f64(double v) {
+  const wx_u64 u = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(wx_u32)u, CTRL, ROW_MASK, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(wx_u32)(u >> 32), CTRL, ROW_MASK, 0xf, false);
+  return __longlong_as_double((long long)(((wx_u64)(wx_u32)hi << 32) | (wx_u32)lo));
+}
+__device__ __forceinline__ double wave_total_f64(double v) {
+  v += dpp_f64<0x111, 0xf>(v);  // row_shr:1
+  v += dpp_f64<0x112, 0xf>(v);  // row_shr:2
+  v += dpp_f64<0x114, 0xf>(v);  // row_shr:4
+  v += dpp_f64<0x118, 0xf>(v);  // row_shr:8
+  v += dpp_f64<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
+  v += dpp_f64<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
+  const wx_u64 u = __double_as_longlong(v);
+  const wx_u32 lo = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)u, 63);
+  const wx_u32 hi = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)(u >> 32), 63);
+  return __longlong_as_double((long long)(((wx_u64)hi << 32) | lo));
+}
+
 // Order-preserving float -> u32 map used by the top-K and sort kernels.
 // -0.0 is canonicalised to +0.0 (they compare equal on the CPU); NaN maps to
 // 0, below every number.

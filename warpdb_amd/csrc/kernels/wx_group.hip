@@ -21,6 +21,9 @@
 #define WX_UNROLL 2
 #endif
 #define WX_HSORT_MAX WX_GROUP_HSORT_MAX
+#ifndef WX_GROUP_LEAD
+#define WX_GROUP_LEAD 16  // lanes of a wave on one window bin from which they add once (0: off)
+#endif
 
 #ifndef WX_MINMAX
 #define WX_MINMAX 0  // also per-group MIN / MAX (NaN skipped)
@@ -83,8 +86,35 @@ extern "C" __global__ __launch_bounds__(WX_GBLOCK) void wx_group_sum(WxGroupArgs
 #endif
   }
   __syncthreads();
+  bool wx_lead_on = false;  // this batch's first rows had a bin shared by many lanes
   WX_STRIDE_LOOP_BEGIN
-  if (idx < wx_a.n_rows && WX_EVAL_COND()) {
+  bool wx_pass = idx < wx_a.n_rows && WX_EVAL_COND();
+#if WX_GROUP_LEAD && !WX_MINMAX
+  // A window bin shared by many lanes of the wave (a skewed key): their values
+  // summed across the wave and added once (the LDS serialises same-address
+  // adds: 90 % of the rows on one key took 7.3 ms per 1e9 rows instead of
+  // 1.2).  Full waves only (the DPP total reads every lane).  Checked on the
+  // first row of each batch, and on every row of a batch whose first row had
+  // such a bin: the check on every row cost the uniform-key C3 query 4.5 %
+  // (profiles/r06/ab_group_lead.txt).
+  if ((wx_u == 0 && wx_e == 0) || wx_lead_on) {
+    const wx_u32 wx_lb = wx_pass ? (wx_u32)(static_cast<int>(WX_KEY) - wx_a.key_lo) : 0xffffffffu;
+    const wx_u32 wx_b0 = (wx_u32)__builtin_amdgcn_readfirstlane((int)wx_lb);
+    const wx_u64 wx_m = __builtin_amdgcn_ballot_w64(wx_lb == wx_b0 && wx_b0 < (wx_u32)WX_GWIN);
+    const bool wx_shared = __builtin_popcountll(wx_m) >= WX_GROUP_LEAD;
+    if (wx_u == 0 && wx_e == 0) wx_lead_on = wx_shared;
+    if (wx_shared && __builtin_amdgcn_read_exec() == ~0ull) {
+      const bool wx_mine = wx_lb == wx_b0;
+      const double wx_t = wx::wave_total_f64(wx_mine ? (double)static_cast<float>(WX_EXPR) : 0.0);
+      if ((threadIdx.x & 63) == __builtin_ctzll(wx_m)) {
+        atomicAdd(&wx_s_sum[wx_b0], wx_t);
+        atomicAdd(&wx_s_cnt[wx_b0], (wx_u32)__builtin_popcountll(wx_m));
+      }
+      wx_pass = wx_pass && !wx_mine;
+    }
+  }
+#endif
+  if (wx_pass) {
     const int wx_key = static_cast<int>(WX_KEY);
     const float wx_val = static_cast<float>(WX_EXPR);
     const wx_u32 wx_bin = (wx_u32)(wx_key - wx_a.key_lo);

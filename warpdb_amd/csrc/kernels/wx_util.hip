@@ -618,30 +618,6 @@ extern "C" __global__ __launch_bounds__(WX_BLOCK) void wx_cast(WxCastArgs a) {
 static_assert(WX_XF_B <= 512, "sums of |q| < 2^44 stay exact doubles for at most 512 values");
 
 namespace wx {
-// Wave total of a double, every lane the same value: an inclusive DPP scan
-// (row shifts, then row broadcasts; no LDS round trips, unlike __shfl_xor's
-// ds_bpermute) and lane 63's result read back.  Exact for the fold's
-// integer-valued sums (< 2^53), so the add order does not matter.
-template <int CTRL, int ROW_MASK>
-__device__ __forceinline__ double dpp_f64(double v) {
-  const wx_u64 u = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(wx_u32)u, CTRL, ROW_MASK, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(wx_u32)(u >> 32), CTRL, ROW_MASK, 0xf, false);
-  return __longlong_as_double((long long)(((wx_u64)(wx_u32)hi << 32) | (wx_u32)lo));
-}
-__device__ __forceinline__ double wave_total_f64(double v) {
-  v += dpp_f64<0x111, 0xf>(v);  // row_shr:1
-  v += dpp_f64<0x112, 0xf>(v);  // row_shr:2
-  v += dpp_f64<0x114, 0xf>(v);  // row_shr:4
-  v += dpp_f64<0x118, 0xf>(v);  // row_shr:8
-  v += dpp_f64<0x142, 0xa>(v);  // row_bcast:15 -> rows 1, 3
-  v += dpp_f64<0x143, 0xc>(v);  // row_bcast:31 -> rows 2, 3
-  const wx_u64 u = __double_as_longlong(v);
-  const wx_u32 lo = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)u, 63);
-  const wx_u32 hi = (wx_u32)__builtin_amdgcn_readlane((int)(wx_u32)(u >> 32), 63);
-  return __longlong_as_double((long long)(((wx_u64)hi << 32) | lo));
-}
-
 // The ties of a row-ordered run of values, 64 at a time (lane l = the l-th
 // value of a row), wave-uniform.  b is rint(q), or floor(q) for a tie; a tie
 // adds b + ((P + b) & 1) where P is the parity of S before it, and leaves S
@@ -684,12 +660,16 @@ struct XfTies {
     cpar = (wx_u32)__builtin_popcountll(pm & ~((2ull << lt) - 1ull)) & 1u;
     seen = 1u;
   }
-  // the first tie's +1 (0 without a tie) once S, the running integer where
-  // the run starts, is known (the rest, t + adj, is formed off the chain)
-  __device__ __forceinline__ double first(double S) const {
-    if (!has) return 0.0;  // wave-uniform
-    const double h = S * 0.5;
-    return (double)((h != __builtin_floor(h) ? 1u : 0u) ^ cf);
+  // S + R for a run of total R (t + adj, formed off the chain) starting at
+  // the running integer S: the first tie's +1 added only when there is a
+  // tie, so a tie-free run puts one add on the chain
+  __device__ __forceinline__ double apply(double S, double R) const {
+    double r = S + R;
+    if (has) {  // wave-uniform
+      const double h = S * 0.5;
+      r += (double)((h != __builtin_floor(h) ? 1u : 0u) ^ cf);
+    }
+    return r;
   }
 };
 
@@ -761,7 +741,7 @@ __device__ __forceinline__ double xf_block(double s, const float (&x)[WX_XF_J], 
       a = wave_total_f64(a);
       const double S = __builtin_ldexp(s, 52 - k);  // the integer s / u, |S| in [2^52, 2^53)
       const bool fits = s > 0.0 ? (S - a > 0x1p52 && S + a < 0x1p53) : (S + a < -0x1p52 && S - a > -0x1p53);
-      if (fits) return __builtin_ldexp(S + (t + T.adj) + T.first(S), k - 52);
+      if (fits) return __builtin_ldexp(T.apply(S, t + T.adj), k - 52);
     }
   }
   const int lane = threadIdx.x & 63;
@@ -843,7 +823,7 @@ __device__ __forceinline__ double fold_exact(const float *v, wx_i64 c, double *l
         const bool fits =
             s > 0.0 ? (S - a[d] > 0x1p52 && S + a[d] < 0x1p53) : (S + a[d] < -0x1p52 && S - a[d] > -0x1p53);
         if (fits) {
-          s = __builtin_ldexp(S + t[d] + T[d].first(S), k - 52);
+          s = __builtin_ldexp(T[d].apply(S, t[d]), k - 52);
           done = true;
         }
       }
