@@ -300,15 +300,17 @@ __device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S,
   }
   __syncthreads();
   // (4) LDS -> output: consecutive threads write consecutive slots of a key's run
+  // each thread clears the counter words it read (slot p's position sits in
+  // counter word p), so one barrier ends the tile
+  static_assert(WX_RO_WAVES / 2 * WX_RO_BINS == WX_RO_ITEMS * WX_RO_BLOCK, "slot p's word is the counter word p");
 #pragma unroll
   for (int j = 0; j < WX_RO_ITEMS; ++j) {
     const wx_u32 p = (wx_u32)(j * WX_RO_BLOCK + tid);
     if (p < n_pass) wx_a.out[(wx_u64)wcf[p]] = s_v[p];
   }
-  __syncthreads();  // every position and value read
 #pragma unroll
-  for (int i = 0; i < WX_RO_WAVES / 2 * WX_RO_BINS / WX_RO_BLOCK; ++i) wcf[i * WX_RO_BLOCK + tid] = 0u;
-  __syncthreads();  // counters zeroed
+  for (int j = 0; j < WX_RO_ITEMS; ++j) wcf[j * WX_RO_BLOCK + tid] = 0u;
+  __syncthreads();  // every position and value read, the counters zeroed
 }
 
 // (Measured and dropped, round 6, profiles/r06/group_row_order_ab.txt: tile
