@@ -169,7 +169,7 @@ __device__ __forceinline__ void wx_ro_eval(const WxRoArgs &wx_a, wx_i64 wb, wx_u
 // Steps (1)-(4) of tile t from its rows' bins and values.
 __device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S, float *s_v,
                                             wx_u32 (&run)[WX_RO_BPT], wx_u32 (&bin)[WX_RO_ITEMS],
-                                            const float (&val)[WX_RO_ITEMS]);
+                                            const float (&val)[WX_RO_ITEMS], wx_i64 t);
 
 template <bool WHOLE>
 __device__ __forceinline__ void wx_ro_tile(const WxRoArgs &wx_a, WxRoShared &S, float *s_v, wx_i64 t,
@@ -184,12 +184,12 @@ __device__ __forceinline__ void wx_ro_tile(const WxRoArgs &wx_a, WxRoShared &S, 
   // otherwise wait for each row's loads in turn to save registers)
   __builtin_amdgcn_sched_barrier(0);
   wx_ro_eval<WHOLE>(wx_a, wb, bin, val, bad WX_COLS(WX_RO_ARG));
-  wx_ro_place(wx_a, S, s_v, run, bin, val);
+  wx_ro_place(wx_a, S, s_v, run, bin, val, t);
 }
 
 __device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S, float *s_v,
                                             wx_u32 (&run)[WX_RO_BPT], wx_u32 (&bin)[WX_RO_ITEMS],
-                                            const float (&val)[WX_RO_ITEMS]) {
+                                            const float (&val)[WX_RO_ITEMS], wx_i64 t) {
   typedef wx_u32 u4 __attribute__((ext_vector_type(4)));
   // an opaque copy of the thread index: the slot and address arithmetic is
   // formed here, not hoisted out of the tile loop into spilled registers
@@ -204,8 +204,11 @@ __device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S,
   // wave's counter (the LDS returns same-address lanes' results in ascending
   // lane order, gfx950); lane 0's bin group adds its size once from lane 0
   // and ranks by its ballot (few keys would serialize on one counter)
+  // (the adds' raw results are unpacked only after all sixteen are issued:
+  // unpacked inside the branch, each add waited for its result before the
+  // next was issued)
   wx_u32 rk[WX_RO_ITEMS];
-  wx_u32 lead_bits = 0u;
+  wx_u32 lead_bits = 0u, atom_bits = 0u;
 #pragma unroll
   for (int i = 0; i < WX_RO_ITEMS; ++i) {
     const bool valid = bin[i] != 0xffffffffu;
@@ -213,12 +216,17 @@ __device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S,
     const bool lead = valid && bin[i] == d0;
     const wx_u64 lm = __builtin_amdgcn_ballot_w64(lead);
     rk[i] = (wx_u32)__builtin_popcountll(lm & below);
-    if (valid && (!lead || lane == 0)) {
+    const bool atom = valid && (!lead || lane == 0);
+    if (atom) {
       const wx_u32 inc = (lead ? (wx_u32)__builtin_popcountll(lm) : 1u) << sh;
-      rk[i] = (atomicAdd(&S.wc[wp][bin[i]], inc) >> sh) & 0xffffu;
+      rk[i] = atomicAdd(&S.wc[wp][bin[i]], inc);  // raw: this wave's half unpacked below
     }
     lead_bits |= (lead && lane != 0 ? 1u : 0u) << i;
+    atom_bits |= (atom ? 1u : 0u) << i;
   }
+#pragma unroll
+  for (int i = 0; i < WX_RO_ITEMS; ++i)
+    if ((atom_bits >> i) & 1u) rk[i] = (rk[i] >> sh) & 0xffffu;
 #pragma unroll
   for (int i = 0; i < WX_RO_ITEMS; ++i) {
     const wx_u32 base0 = __builtin_amdgcn_readlane(rk[i], 0);
@@ -287,15 +295,21 @@ __device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S,
   __syncthreads();
   // (3) slots; then the values into bin order in LDS and, in the counters'
   // place, each slot's output position
+  // (reads unconditional -- a row that does not pass reads bin 0 -- so they
+  // are all issued before the first result is waited for)
+  wx_u32 gbv[WX_RO_ITEMS];
 #pragma unroll
-  for (int i = 0; i < WX_RO_ITEMS; ++i)
-    if (bin[i] != 0xffffffffu) rk[i] += (S.wc[wp][bin[i]] >> sh) & 0xffffu;
+  for (int i = 0; i < WX_RO_ITEMS; ++i) {
+    const wx_u32 bb = bin[i] != 0xffffffffu ? bin[i] : 0u;
+    rk[i] += (S.wc[wp][bb] >> sh) & 0xffffu;
+    gbv[i] = S.gb[bb];
+  }
   __syncthreads();  // every slot base read: the positions take the counters' place
 #pragma unroll
   for (int i = 0; i < WX_RO_ITEMS; ++i) {
     if (bin[i] != 0xffffffffu) {
       s_v[rk[i]] = val[i];
-      wcf[rk[i]] = S.gb[bin[i]] + rk[i];
+      wcf[rk[i]] = gbv[i] + rk[i];
     }
   }
   __syncthreads();
@@ -303,11 +317,32 @@ __device__ __forceinline__ void wx_ro_place(const WxRoArgs &wx_a, WxRoShared &S,
   // each thread clears the counter words it read (slot p's position sits in
   // counter word p), so one barrier ends the tile
   static_assert(WX_RO_WAVES / 2 * WX_RO_BINS == WX_RO_ITEMS * WX_RO_BLOCK, "slot p's word is the counter word p");
+  // (every slot's position and value read first -- unconditionally, so the
+  // reads are all in flight together -- then the passing slots stored)
+  wx_u32 pos[WX_RO_ITEMS];
+  float sv[WX_RO_ITEMS];
 #pragma unroll
   for (int j = 0; j < WX_RO_ITEMS; ++j) {
-    const wx_u32 p = (wx_u32)(j * WX_RO_BLOCK + tid);
-    if (p < n_pass) wx_a.out[(wx_u64)wcf[p]] = s_v[p];
+    pos[j] = wcf[j * WX_RO_BLOCK + tid];
+    sv[j] = s_v[j * WX_RO_BLOCK + tid];
   }
+#if !defined(WX_RO_DIAG_STORE) || !WX_DIAG
+// diagnostic (a WX_DIAG build only): 1 = each tile's values stored to its
+// own rows' places (coalesced, wrong order), 2 = no stores
+#undef WX_RO_DIAG_STORE
+#define WX_RO_DIAG_STORE 0
+#endif
+#pragma unroll
+  for (int j = 0; j < WX_RO_ITEMS; ++j)
+    if ((wx_u32)(j * WX_RO_BLOCK + tid) < n_pass) {
+#if WX_RO_DIAG_STORE == 1
+      wx_a.out[(wx_u64)t * WX_RO_TILE + j * WX_RO_BLOCK + tid] = sv[j];
+#elif WX_RO_DIAG_STORE == 2
+      if (sv[j] == -1.2345f) wx_a.out[(wx_u64)pos[j]] = sv[j];
+#else
+      wx_a.out[(wx_u64)pos[j]] = sv[j];
+#endif
+    }
 #pragma unroll
   for (int j = 0; j < WX_RO_ITEMS; ++j) wcf[j * WX_RO_BLOCK + tid] = 0u;
   __syncthreads();  // every position and value read, the counters zeroed
