@@ -262,3 +262,30 @@ def test_row_order_big_group_chunked(path, values):
         want = np.add.accumulate(v[q == k[i]].astype(np.float64))[-1]
         assert c[i] == int((q == k[i]).sum())
         assert bits(s[i]) == bits(want), (i, s[i], want)
+
+
+@pytest.mark.parametrize("lo,width", [(0, 2048), (0, 2049), (2**31 - 2048, 2048), (-2**31, 2048), (-2**31, 2049),
+                                      (-1024, 2048)])
+@pytest.mark.parametrize("mode", ["span", "ordinary"])
+def test_row_order_key_span_boundaries(lo, width, mode, monkeypatch):
+    """Keys spanning exactly the 2048 bins of the key-span scatter (at 0, at
+    the int32 extremes, straddling 0) take it; one key more takes the
+    general path.  The lowest and highest key each appear once, in the
+    middle of the table (a strided sample misses them: the direct path's
+    miss flag and fallback at the int32 extremes), and a WHERE drops rows.
+    Equal to the oracle's sequential fold bit for bit."""
+    monkeypatch.setenv("WARPDB_GROUP_ROWS", mode)
+    n = 300_007
+    rng = np.random.default_rng(lo % 1000 + width)
+    q = rng.integers(lo + 1, lo + width - 1, n, dtype=np.int64)
+    q[n // 2 + 3] = lo
+    q[n // 2 + 5] = lo + width - 1
+    cols = {"price": spread_values(rng, n), "quantity": q.astype(np.int32)}
+    cols["price"][n // 2 + 3] = 3.0  # the extreme keys' rows pass the WHERE
+    cols["price"][n // 2 + 5] = 4.0
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", "price > 0.25", capacity=4096)
+    assert rk[0] == lo and rk[-1] == lo + width - 1
+    for _ in range(2):  # the second call takes the memo's range
+        g, k, s, c = run(cols, "(price[idx] > 0.25f)", 4096)
+        assert g == len(rk) and np.array_equal(k, rk) and np.array_equal(c, rc)
+        assert np.array_equal(bits(s), bits(rs))
