@@ -289,3 +289,38 @@ def test_row_order_key_span_boundaries(lo, width, mode, monkeypatch):
         g, k, s, c = run(cols, "(price[idx] > 0.25f)", 4096)
         assert g == len(rk) and np.array_equal(k, rk) and np.array_equal(c, rc)
         assert np.array_equal(bits(s), bits(rs))
+
+
+@pytest.mark.parametrize("kind", ["int_expr", "float_col", "int_col", "int_col_where"])
+def test_row_order_general_key_sources(kind, monkeypatch):
+    """The general path's keys: a bare int32 key column with no WHERE is
+    sorted straight from the column (no key projection); a key expression,
+    a float key column (cast to int) or a WHERE go through the key
+    compaction.  Groups of every size class: one lane each (<= 4096 rows),
+    one wave each, and (with WARPDB_FOLD_SMALL=0) one wave for all.  Equal
+    to the oracle's sequential fold bit for bit."""
+    n = 700_001
+    rng = np.random.default_rng(61)
+    q = rng.integers(0, 50_000, n).astype(np.int32)
+    q[rng.random(n) < 0.3] = 12_345  # one group of ~210 000 rows (a wave), the rest ~10 rows (lanes)
+    cols = {"price": spread_values(rng, n), "quantity": q}
+    key_gpu, key_ora, cond_gpu, cond_ora = "quantity[idx]", "quantity", None, None
+    if kind == "int_expr":
+        key_gpu, key_ora = "(quantity[idx] * 3)", "quantity * 3"
+    elif kind == "float_col":
+        cols["quantity"] = q.astype(np.float32)
+    elif kind == "int_col_where":
+        cond_gpu, cond_ora = "(price[idx] > 0.25f)", "price > 0.25"
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", key_ora, cond_ora, capacity=1 << 17)
+    t, _ = dev_table(cols)
+    cap = 1 << 17
+    for small in ("", "0"):
+        monkeypatch.setenv("WARPDB_FOLD_SMALL", small)
+        keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+        sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+        cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+        g = wx.group_sum(t, "price[idx]", key_gpu, cond_gpu, launch(), 0, cap, keys.data_ptr(), sums.data_ptr(),
+                         cnts.data_ptr())
+        assert g == len(rk)
+        assert np.array_equal(keys[:g].cpu().numpy(), rk) and np.array_equal(cnts[:g].cpu().numpy(), rc)
+        assert np.array_equal(bits(sums[:g].cpu().numpy()), bits(rs)), small

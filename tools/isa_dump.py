@@ -36,7 +36,7 @@ subprocess.run(["hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-con
                 "--cuda-device-only", "-S", "-o", asm, hip], check=True)
 text = open(asm).read()
 for kern in re.findall(r"\.amdhsa_kernel (\w+)", text):
-    blk = text.split(f".amdhsa_kernel {kern}", 1)
+    blk = text.split(f".amdhsa_kernel {kern}\n", 1)
     if len(blk) < 2:
         continue
     meta = blk[1].split(".end_amdhsa_kernel", 1)[0]

@@ -359,7 +359,18 @@ struct WxGroupFoldArgs {
   double *out_sums;        // [n_groups]
   wx_u64 *ctrs;            // [1]: error bits (a group whose rows do not match its count)
   wx_i64 skip_above;       // > 0: groups of more rows are folded by the wx_xf_big_* kernels instead
+  wx_i64 *starts;          // [n_groups] each group's first row in the sorted arrays (the counts' exclusive prefix)
+  wx_i64 *chunk_sums;      // [n_chunks] the counts' sums per WX_GS_CHUNK groups, then their exclusive prefix
+  wx_i64 n_chunks;
+  wx_i64 small_max;        // groups of at most this many rows: one lane each (wx_group_fold_small)
+  wx_i64 *big_list;        // [n_groups] the other groups, for wx_group_fold (one wave each), in any order
+  wx_u32 *big_n;           // [1] their number (zeroed before wx_group_fold_small)
 };
+// wx_group_starts_*: WX_GS_BLOCK threads, WX_GS_PER consecutive groups each
+#define WX_GS_BLOCK 256
+#define WX_GS_PER 16
+#define WX_GS_CHUNK (WX_GS_BLOCK * WX_GS_PER)
+#define WX_FOLD_SMALL 4096
 
 // Row-order folds of groups larger than WX_XF_BIG rows, split into chunks of
 // WX_XF_CHUNK values (wx_xf_big_approx / _exact / _combine, wx_util.hip).

@@ -990,15 +990,150 @@ extern "C" __global__ __launch_bounds__(64) void wx_xf_big_combine(WxXfBigArgs a
   }
 }
 
-// Row-order GROUP BY sums (WX_F_ROW_ORDER, warpexec.cpp do_group_sum_rows):
-// one wave per group.  The wave finds the group's first row in the
-// key-sorted array (lower bound), checks that exactly its count of rows
-// carry the key, and folds their values in ascending row order, one
-// dependent double add per row -- the reference's std::map fold
-// (src/warpdb.cpp:373-385) to the bit.  The lanes stream the group's values
-// (coalesced, WX_FOLD_U chunks of 64 in flight); the chain runs over them in
-// lane order (LDS broadcasts, or v_readlane with WX_FOLD_LDS=0), so every
-// lane holds the same running sum.
+// Row-order GROUP BY sums, general path (WX_F_ROW_ORDER, warpexec.cpp
+// do_group_sum_rows): the passing rows sorted by key, row order kept within
+// a key, so group g's rows are [starts[g], starts[g] + count[g]) -- the
+// counts' exclusive prefix, since the groups come in ascending key order and
+// the sorted array holds exactly their rows (wx_group_starts_* form it and
+// check that the counts add up to the rows).  Then each group's values are
+// folded in ascending row order -- the reference's std::map fold
+// (src/warpdb.cpp:373-385: `g.sum += val`) to the bit -- small groups one
+// lane each (wx_group_fold_small), the rest one wave each (wx_group_fold),
+// groups above skip_above in chunks (wx_xf_big_*).  (Before round 6 each
+// wave found its group's first row by a binary search of the sorted keys:
+// 30 dependent loads per group, 9.1 ms of the 33.6-ms query at 10^6 keys.)
+
+// exclusive prefix over a workgroup of WX_GS_BLOCK threads (s_w: one word
+// per wave); the total in tot
+__device__ __forceinline__ wx_i64 wx_gs_block_excl(wx_i64 v, wx_i64 *s_w, wx_i64 &tot) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  wx_i64 incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const wx_i64 t = __shfl_up(incl, o);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) s_w[wave] = incl;
+  __syncthreads();
+  wx_i64 wb = 0;
+  tot = 0;
+#pragma unroll
+  for (int w = 0; w < WX_GS_BLOCK / 64; ++w) {
+    const wx_i64 x = s_w[w];
+    wb += w < wave ? x : 0;
+    tot += x;
+  }
+  __syncthreads();  // s_w reusable
+  return wb + incl - v;
+}
+
+// (1) chunk b's count total: groups [b * WX_GS_CHUNK, ...), WX_GS_PER per thread
+extern "C" __global__ __launch_bounds__(WX_GS_BLOCK) void wx_group_starts_sum(WxGroupFoldArgs a) {
+  __shared__ wx_i64 s_w[WX_GS_BLOCK / 64];
+  const wx_i64 g0 = (wx_i64)blockIdx.x * WX_GS_CHUNK + (wx_i64)threadIdx.x * WX_GS_PER;
+  wx_i64 v = 0;
+#pragma unroll
+  for (int k = 0; k < WX_GS_PER; ++k)
+    if (g0 + k < a.n_groups) v += a.gcounts[g0 + k];
+  wx_i64 tot;
+  wx_gs_block_excl(v, s_w, tot);
+  if (threadIdx.x == 0) a.chunk_sums[blockIdx.x] = tot;
+}
+
+// (2) the chunk totals' exclusive prefix, in place (one 1024-thread
+// workgroup, 1024 chunks per round); the rows must add up to m
+extern "C" __global__ __launch_bounds__(1024) void wx_group_starts_scan(WxGroupFoldArgs a) {
+  __shared__ wx_i64 s_w[16];
+  __shared__ wx_i64 s_carry;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (wx_i64 base = 0; base < a.n_chunks; base += 1024) {
+    const wx_i64 i = base + tid;
+    const wx_i64 v = i < a.n_chunks ? a.chunk_sums[i] : 0;
+    wx_i64 incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_i64 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    wx_i64 wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 16; ++w) {
+      const wx_i64 x = s_w[w];
+      wb += w < wave ? x : 0;
+      tot += x;
+    }
+    const wx_i64 carry = s_carry;
+    if (i < a.n_chunks) a.chunk_sums[i] = carry + wb + incl - v;
+    __syncthreads();
+    if (tid == 0) s_carry = carry + tot;
+    __syncthreads();
+  }
+  if (tid == 0 && s_carry != a.m) {  // the counts do not cover the sorted rows exactly
+    atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+  }
+}
+
+// (3) every group's first row: chunk prefix + the prefix inside the chunk
+extern "C" __global__ __launch_bounds__(WX_GS_BLOCK) void wx_group_starts_emit(WxGroupFoldArgs a) {
+  __shared__ wx_i64 s_w[WX_GS_BLOCK / 64];
+  const wx_i64 g0 = (wx_i64)blockIdx.x * WX_GS_CHUNK + (wx_i64)threadIdx.x * WX_GS_PER;
+  wx_i64 c[WX_GS_PER], v = 0;
+#pragma unroll
+  for (int k = 0; k < WX_GS_PER; ++k) {
+    c[k] = g0 + k < a.n_groups ? a.gcounts[g0 + k] : 0;
+    v += c[k];
+  }
+  wx_i64 tot;
+  wx_i64 p = a.chunk_sums[blockIdx.x] + wx_gs_block_excl(v, s_w, tot);
+#pragma unroll
+  for (int k = 0; k < WX_GS_PER; ++k) {
+    if (g0 + k < a.n_groups) a.starts[g0 + k] = p;
+    p += c[k];
+  }
+}
+
+// (4) one lane per group of at most small_max rows: the plain sequential
+// fold, eight values loaded ahead of their adds; a larger group goes to
+// big_list for wx_group_fold.  Every group's first and last sorted key must
+// be its key (with the counts adding up to the rows, checked in (2), that
+// pins every group's rows).
+extern "C" __global__ __launch_bounds__(WX_GS_BLOCK) void wx_group_fold_small(WxGroupFoldArgs a) {
+  const wx_i64 g = (wx_i64)blockIdx.x * WX_GS_BLOCK + threadIdx.x;
+  if (g >= a.n_groups) return;
+  const wx_i64 c = a.gcounts[g], lo = a.starts[g];
+  if (c > a.small_max) {
+    a.big_list[atomicAdd(a.big_n, 1u)] = g;
+    return;
+  }
+  const int key = a.gkeys[g];
+  if (c < 1 || lo < 0 || lo + c > a.m || a.skeys[lo] != key || a.skeys[lo + c - 1] != key) {
+    atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
+    a.out_sums[g] = 0.0;
+    return;
+  }
+  const float *v = a.svals + lo;
+  double s = 0.0;
+  wx_i64 i = 0;
+  for (; i + 8 <= c; i += 8) {
+    float x[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) x[u] = v[i + u];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) s += (double)x[u];
+  }
+  for (; i < c; ++i) s += (double)v[i];
+  a.out_sums[g] = s;
+}
+
+// (5) one wave per group of big_list (every group when big_list is null),
+// by wx::fold_exact; with WX_FOLD_EXACT=0 the lanes stream the group's
+// values (coalesced, WX_FOLD_U chunks of 64 in flight) and the chain runs
+// over them in lane order (LDS broadcasts, or v_readlane with
+// WX_FOLD_LDS=0), so every lane holds the same running sum.
 // A chunk past the group's end is padded with +0.0, which leaves any running
 // sum unchanged (the sum starts at +0.0, so it is never -0.0).  1e9 rows x
 // 1024 keys: 11.4 ms through LDS broadcasts (about 11 ns per dependent
@@ -1013,16 +1148,12 @@ extern "C" __global__ __launch_bounds__(64) void wx_xf_big_combine(WxXfBigArgs a
 extern "C" __global__ __launch_bounds__(64) void wx_group_fold(WxGroupFoldArgs a) {
   const int lane = threadIdx.x;
   __shared__ double s_fold[64];
-  for (wx_i64 g = blockIdx.x; g < a.n_groups; g += gridDim.x) {
+  const wx_i64 n_items = a.big_list ? (wx_i64)*a.big_n : a.n_groups;
+  for (wx_i64 it = blockIdx.x; it < n_items; it += gridDim.x) {
+    const wx_i64 g = a.big_list ? a.big_list[it] : it;
     const int key = a.gkeys[g];
-    const wx_i64 c = a.gcounts[g];
-    wx_i64 lo = 0, hi = a.m;
-    while (lo < hi) {
-      const wx_i64 mid = (lo + hi) >> 1;
-      if (a.skeys[mid] < key) lo = mid + 1;
-      else hi = mid;
-    }
-    if (c < 1 || lo + c > a.m || a.skeys[lo + c - 1] != key || (lo + c < a.m && a.skeys[lo + c] == key)) {
+    const wx_i64 c = a.gcounts[g], lo = a.starts[g];
+    if (c < 1 || lo < 0 || lo + c > a.m || a.skeys[lo] != key || a.skeys[lo + c - 1] != key) {
       if (lane == 0) {
         atomicOr(reinterpret_cast<unsigned int *>(&a.ctrs[1]), WX_DEVERR_INTERNAL_KEY);
         a.out_sums[g] = 0.0;
