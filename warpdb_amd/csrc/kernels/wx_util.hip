@@ -1115,15 +1115,27 @@ extern "C" __global__ __launch_bounds__(WX_GS_BLOCK) void wx_group_fold_small(Wx
     a.out_sums[g] = 0.0;
     return;
   }
+  // the lanes' groups lie apart, so each load instruction touches 64 lines:
+  // 16-B loads (after up to three values to a 16-B boundary) need a quarter
+  // of the instructions that 4-B loads do
+  typedef float f4 __attribute__((ext_vector_type(4)));
   const float *v = a.svals + lo;
   double s = 0.0;
+  const wx_i64 head = c < (wx_i64)((4u - ((wx_u32)(reinterpret_cast<wx_u64>(v) >> 2) & 3u)) & 3u)
+                          ? c
+                          : (wx_i64)((4u - ((wx_u32)(reinterpret_cast<wx_u64>(v) >> 2) & 3u)) & 3u);
   wx_i64 i = 0;
+  for (; i < head; ++i) s += (double)v[i];
   for (; i + 8 <= c; i += 8) {
-    float x[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) x[u] = v[i + u];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) s += (double)x[u];
+    const f4 x0 = *reinterpret_cast<const f4 *>(v + i), x1 = *reinterpret_cast<const f4 *>(v + i + 4);
+    s += (double)x0.x;
+    s += (double)x0.y;
+    s += (double)x0.z;
+    s += (double)x0.w;
+    s += (double)x1.x;
+    s += (double)x1.y;
+    s += (double)x1.z;
+    s += (double)x1.w;
   }
   for (; i < c; ++i) s += (double)v[i];
   a.out_sums[g] = s;
