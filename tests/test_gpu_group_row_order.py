@@ -324,3 +324,24 @@ def test_row_order_general_key_sources(kind, monkeypatch):
         assert g == len(rk)
         assert np.array_equal(keys[:g].cpu().numpy(), rk) and np.array_equal(cnts[:g].cpu().numpy(), rc)
         assert np.array_equal(bits(sums[:g].cpu().numpy()), bits(rs)), small
+
+
+@pytest.mark.parametrize("mode", ["span", "general", "ordinary"])
+def test_row_order_wide_keys_capacity_and_empty(mode, monkeypatch):
+    """Keys spanning more than 2048 take the general path; without MIN / MAX
+    and no ordinary call (span / general modes) its groups come from the
+    sorted keys' runs.  More groups than the capacity is the ordinary call's
+    capacity error, and a WHERE nothing passes gives no groups, on every
+    route."""
+    monkeypatch.setenv("WARPDB_GROUP_ROWS", mode)
+    n = 200_003
+    rng = np.random.default_rng(67)
+    cols = {"price": spread_values(rng, n), "quantity": (rng.integers(0, 5000, n) * 7).astype(np.int32)}
+    with pytest.raises(wx.WarpExecError):
+        run(cols, None, 100)
+    g, *_ = run(cols, "(price[idx] < -1.0f)", 100)
+    assert g == 0
+    g, k, s, c = run(cols, None, 8192)
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", capacity=8192)
+    assert g == len(rk) and np.array_equal(k, rk) and np.array_equal(c, rc)
+    assert np.array_equal(bits(s), bits(rs))

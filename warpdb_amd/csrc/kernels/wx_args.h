@@ -366,6 +366,24 @@ struct WxGroupFoldArgs {
   wx_i64 *big_list;        // [n_groups] the other groups, for wx_group_fold (one wave each), in any order
   wx_u32 *big_n;           // [1] their number (zeroed before wx_group_fold_small)
 };
+// The groups of a key-sorted array by run-length encoding (the general
+// row-order path without the ordinary call): wx_rle_count / _scan / _emit /
+// _counts.  Wave r of n_blk (WX_RLE_BLOCK / 64 per workgroup) takes rows
+// [r * span, (r + 1) * span), span a multiple of 64.
+struct WxRleArgs {
+  const int *sk;           // [m] sorted keys
+  wx_i64 m;
+  wx_i64 span;             // rows per wave
+  int n_blk;               // wave ranges
+  wx_i64 *blk;             // [n_blk] runs starting in each wave's rows, then their exclusive prefix
+  wx_i64 *n_out;           // [1] the runs (groups)
+  wx_i64 *n_groups_out;    // the caller's group count (nullable)
+  wx_i64 capacity;         // outputs beyond it are not written
+  int *out_keys;           // [capacity] each run's key, ascending
+  wx_i64 *out_counts;      // [capacity] its length
+  wx_i64 *starts;          // [capacity] its first row
+};
+#define WX_RLE_BLOCK 1024
 // wx_group_starts_*: WX_GS_BLOCK threads, WX_GS_PER consecutive groups each
 #define WX_GS_BLOCK 256
 #define WX_GS_PER 16

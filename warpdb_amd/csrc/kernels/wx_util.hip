@@ -1141,6 +1141,113 @@ extern "C" __global__ __launch_bounds__(WX_GS_BLOCK) void wx_group_fold_small(Wx
   a.out_sums[g] = s;
 }
 
+// Run-length encoding of the sorted keys (the general path's groups when
+// no ordinary call ran): a run starts at row i when i == 0 or the key
+// differs from row i - 1's.  Every wave walks its own range in 64-row
+// chunks, WX_RLE_U of them in flight: no barriers.
+#define WX_RLE_U 8
+// the head flags of rows c + u * 64 + lane, u < WX_RLE_U (rows >= e: none)
+__device__ __forceinline__ void wx_rle_heads(const WxRleArgs &a, wx_i64 c, wx_i64 e, bool (&h)[WX_RLE_U]) {
+  const int lane = threadIdx.x & 63;
+  int k[WX_RLE_U], p[WX_RLE_U];
+#pragma unroll
+  for (int u = 0; u < WX_RLE_U; ++u) {
+    const wx_i64 i = c + u * 64 + lane;
+    k[u] = i < e ? a.sk[i] : 0;
+    // lane 0's predecessor is the previous chunk's lane 63 (row i - 1)
+    p[u] = lane == 0 && i > 0 && i < e ? a.sk[i - 1] : 0;
+  }
+#pragma unroll
+  for (int u = 0; u < WX_RLE_U; ++u) {
+    const wx_i64 i = c + u * 64 + lane;
+    const int prev = __shfl_up(k[u], 1);
+    h[u] = i < e && (i == 0 || k[u] != (lane == 0 ? p[u] : prev));
+  }
+}
+
+// (R1) the runs starting in each wave's rows
+extern "C" __global__ __launch_bounds__(WX_RLE_BLOCK) void wx_rle_count(WxRleArgs a) {
+  const wx_i64 r = (wx_i64)blockIdx.x * (WX_RLE_BLOCK / 64) + (threadIdx.x >> 6);
+  if (r >= a.n_blk) return;  // wave-uniform
+  const wx_i64 b0 = r * a.span, b1 = b0 + a.span < a.m ? b0 + a.span : a.m;
+  wx_i64 n = 0;
+  for (wx_i64 c = b0; c < b1; c += 64 * WX_RLE_U) {
+    bool h[WX_RLE_U];
+    wx_rle_heads(a, c, b1, h);
+#pragma unroll
+    for (int u = 0; u < WX_RLE_U; ++u) n += __builtin_popcountll(__builtin_amdgcn_ballot_w64(h[u]));
+  }
+  if ((threadIdx.x & 63) == 0) a.blk[r] = n;
+}
+
+// (R2) their exclusive prefix (one workgroup, WX_RLE_BLOCK ranges per round) and the total
+extern "C" __global__ __launch_bounds__(WX_RLE_BLOCK) void wx_rle_scan(WxRleArgs a) {
+  __shared__ wx_i64 s_w[WX_RLE_BLOCK / 64];
+  __shared__ wx_i64 s_carry;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (wx_i64 base = 0; base < a.n_blk; base += WX_RLE_BLOCK) {  // workgroup-uniform
+    const wx_i64 i = base + tid;
+    const wx_i64 v = i < a.n_blk ? a.blk[i] : 0;
+    wx_i64 incl = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const wx_i64 t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    if (lane == 63) s_w[wave] = incl;
+    __syncthreads();
+    wx_i64 wb = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < WX_RLE_BLOCK / 64; ++w) {
+      const wx_i64 x = s_w[w];
+      wb += w < wave ? x : 0;
+      tot += x;
+    }
+    const wx_i64 carry = s_carry;
+    if (i < a.n_blk) a.blk[i] = carry + wb + incl - v;
+    __syncthreads();  // s_w and s_carry read
+    if (tid == 0) s_carry = carry + tot;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    a.n_out[0] = s_carry;
+    if (a.n_groups_out) a.n_groups_out[0] = s_carry;
+  }
+}
+
+// (R3) each run's key and first row, in order (runs past capacity not written)
+extern "C" __global__ __launch_bounds__(WX_RLE_BLOCK) void wx_rle_emit(WxRleArgs a) {
+  const wx_i64 r = (wx_i64)blockIdx.x * (WX_RLE_BLOCK / 64) + (threadIdx.x >> 6);
+  if (r >= a.n_blk) return;  // wave-uniform
+  const wx_i64 b0 = r * a.span, b1 = b0 + a.span < a.m ? b0 + a.span : a.m;
+  wx_i64 base = a.blk[r];
+  for (wx_i64 c = b0; c < b1; c += 64 * WX_RLE_U) {
+    bool h[WX_RLE_U];
+    wx_rle_heads(a, c, b1, h);
+#pragma unroll
+    for (int u = 0; u < WX_RLE_U; ++u) {
+      const wx_u64 m = __builtin_amdgcn_ballot_w64(h[u]);
+      if (h[u]) {
+        const wx_i64 q = base + (wx_i64)::wx::lanes_below(m), i = c + u * 64 + (threadIdx.x & 63);
+        if (q < a.capacity) {
+          a.out_keys[q] = a.sk[i];
+          a.starts[q] = i;
+        }
+      }
+      base += __builtin_popcountll(m);
+    }
+  }
+}
+
+// (R4) each run's length: the next run's first row (or m) minus its own
+extern "C" __global__ __launch_bounds__(WX_GS_BLOCK) void wx_rle_counts(WxRleArgs a) {
+  const wx_i64 ng = a.n_out[0], r = (wx_i64)blockIdx.x * WX_GS_BLOCK + threadIdx.x;
+  if (r >= ng || r >= a.capacity) return;
+  a.out_counts[r] = (r + 1 < ng ? a.starts[r + 1] : a.m) - a.starts[r];
+}
+
 // (5) one wave per group of big_list (every group when big_list is null),
 // by wx::fold_exact; with WX_FOLD_EXACT=0 the lanes stream the group's
 // values (coalesced, WX_FOLD_U chunks of 64 in flight) and the chain runs
