@@ -1126,16 +1126,29 @@ extern "C" __global__ __launch_bounds__(WX_GS_BLOCK) void wx_group_fold_small(Wx
                           : (wx_i64)((4u - ((wx_u32)(reinterpret_cast<wx_u64>(v) >> 2) & 3u)) & 3u);
   wx_i64 i = 0;
   for (; i < head; ++i) s += (double)v[i];
-  for (; i + 8 <= c; i += 8) {
-    const f4 x0 = *reinterpret_cast<const f4 *>(v + i), x1 = *reinterpret_cast<const f4 *>(v + i + 4);
-    s += (double)x0.x;
-    s += (double)x0.y;
-    s += (double)x0.z;
-    s += (double)x0.w;
-    s += (double)x1.x;
-    s += (double)x1.y;
-    s += (double)x1.z;
-    s += (double)x1.w;
+  // 16 values per step, the next step's four loads issued before this
+  // step's adds (two steps in flight)
+  if (i + 16 <= c) {
+    f4 n[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) n[q] = *reinterpret_cast<const f4 *>(v + i + 4 * q);
+    for (;;) {
+      const f4 x[4] = {n[0], n[1], n[2], n[3]};
+      const bool more = i + 32 <= c;
+      if (more) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) n[q] = *reinterpret_cast<const f4 *>(v + i + 16 + 4 * q);
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s += (double)x[q].x;
+        s += (double)x[q].y;
+        s += (double)x[q].z;
+        s += (double)x[q].w;
+      }
+      i += 16;
+      if (!more) break;
+    }
   }
   for (; i < c; ++i) s += (double)v[i];
   a.out_sums[g] = s;
