@@ -291,12 +291,14 @@ def test_row_order_key_span_boundaries(lo, width, mode, monkeypatch):
         assert np.array_equal(bits(s), bits(rs))
 
 
-@pytest.mark.parametrize("kind", ["int_expr", "float_col", "int_col", "int_col_where"])
+@pytest.mark.parametrize("kind", ["int_expr", "float_col", "int_col", "int_col_where", "val_expr", "int_val"])
 def test_row_order_general_key_sources(kind, monkeypatch):
-    """The general path's keys: a bare int32 key column with no WHERE is
-    sorted straight from the column (no key projection); a key expression,
-    a float key column (cast to int) or a WHERE go through the key
-    compaction.  Groups of every size class: one lane each (<= 4096 rows),
+    """The general path's keys and values: a bare int32 key column with no
+    WHERE is sorted straight from the column (no key projection), a bare
+    float32 value column with no WHERE rides as the sort's payload straight
+    from the column (no value projection); a key expression, a float key
+    column (cast to int), a value expression, an int value column (converted
+    to float) or a WHERE go through the compactions.  Groups of every size class: one lane each (<= 4096 rows),
     one wave each, and (with WARPDB_FOLD_SMALL=0) one wave for all.  Equal
     to the oracle's sequential fold bit for bit."""
     n = 700_001
@@ -305,13 +307,19 @@ def test_row_order_general_key_sources(kind, monkeypatch):
     q[rng.random(n) < 0.3] = 12_345  # one group of ~210 000 rows (a wave), the rest ~10 rows (lanes)
     cols = {"price": spread_values(rng, n), "quantity": q}
     key_gpu, key_ora, cond_gpu, cond_ora = "quantity[idx]", "quantity", None, None
+    val_gpu, val_ora = "price[idx]", "price"
+    if kind == "val_expr":
+        val_gpu, val_ora = "(price[idx] * 3.0f)", "price * 3"
+    elif kind == "int_val":
+        cols["units"] = rng.integers(-1000, 1000, n).astype(np.int32)
+        val_gpu, val_ora = "units[idx]", "units"
     if kind == "int_expr":
         key_gpu, key_ora = "(quantity[idx] * 3)", "quantity * 3"
     elif kind == "float_col":
         cols["quantity"] = q.astype(np.float32)
     elif kind == "int_col_where":
         cond_gpu, cond_ora = "(price[idx] > 0.25f)", "price > 0.25"
-    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", key_ora, cond_ora, capacity=1 << 17)
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), val_ora, key_ora, cond_ora, capacity=1 << 17)
     t, _ = dev_table(cols)
     cap = 1 << 17
     for small in ("", "0"):
@@ -319,7 +327,7 @@ def test_row_order_general_key_sources(kind, monkeypatch):
         keys = torch.empty(cap, dtype=torch.int32, device="cuda")
         sums = torch.empty(cap, dtype=torch.float64, device="cuda")
         cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
-        g = wx.group_sum(t, "price[idx]", key_gpu, cond_gpu, launch(), 0, cap, keys.data_ptr(), sums.data_ptr(),
+        g = wx.group_sum(t, val_gpu, key_gpu, cond_gpu, launch(), 0, cap, keys.data_ptr(), sums.data_ptr(),
                          cnts.data_ptr())
         assert g == len(rk)
         assert np.array_equal(keys[:g].cpu().numpy(), rk) and np.array_equal(cnts[:g].cpu().numpy(), rc)
