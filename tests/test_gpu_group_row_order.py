@@ -353,3 +353,40 @@ def test_row_order_wide_keys_capacity_and_empty(mode, monkeypatch):
     rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", capacity=8192)
     assert g == len(rk) and np.array_equal(k, rk) and np.array_equal(c, rc)
     assert np.array_equal(bits(s), bits(rs))
+
+
+def test_shutdown_releases_every_workspace_buffer():
+    """wx_shutdown frees every buffer the workspaces allocated (it once freed
+    a fixed list that missed the partitioned GROUP BY's staging, the group
+    lists and the row-order fold's buffers), and the library works again
+    afterwards.  The row-order general path (keys spanning > 2048) holds
+    ≈ 16 B per row (sorted keys and values, the sort's scratch), the
+    partitioned GROUP BY (10^5 keys, capacity > 4096) 6 B per row of
+    staging: at least 20 B per row must come back."""
+    lib = wx.load()
+    n = 16_000_003
+    rng = np.random.default_rng(71)
+    cols = {"price": rng.uniform(0, 40, n).astype(np.float32),
+            "quantity": rng.integers(0, 100_000, n).astype(np.int32)}
+    t, _ = dev_table(cols)
+    cap = 1 << 17
+    keys = torch.empty(cap, dtype=torch.int32, device="cuda")
+    sums = torch.empty(cap, dtype=torch.float64, device="cuda")
+    cnts = torch.empty(cap, dtype=torch.int64, device="cuda")
+
+    def query(flags):
+        return wx.group_sum(t, "price[idx]", "quantity[idx]", None, launch(flags), 0, cap, keys.data_ptr(),
+                            sums.data_ptr(), cnts.data_ptr())
+
+    g_plain = query(0)
+    g_rows = query(wx.F_ROW_ORDER)
+    assert g_plain == g_rows == len(np.unique(cols["quantity"]))
+    torch.cuda.synchronize()
+    free_before = torch.cuda.mem_get_info()[0]
+    lib.wx_shutdown()
+    torch.cuda.synchronize()
+    free_after = torch.cuda.mem_get_info()[0]
+    assert free_after - free_before >= 20 * n, (free_before, free_after)
+    s_before = sums[:g_rows].clone()
+    assert query(wx.F_ROW_ORDER) == g_rows  # the workspaces and modules come back
+    assert torch.equal(sums[:g_rows].view(torch.int64), s_before.view(torch.int64))
