@@ -390,3 +390,17 @@ def test_shutdown_releases_every_workspace_buffer():
     s_before = sums[:g_rows].clone()
     assert query(wx.F_ROW_ORDER) == g_rows  # the workspaces and modules come back
     assert torch.equal(sums[:g_rows].view(torch.int64), s_before.view(torch.int64))
+
+
+@pytest.mark.parametrize("rows", [1, 2, 63, 64, 65])
+def test_row_order_general_tiny_tables(rows, monkeypatch):
+    """The general path's run-length encoding and folds at tables of one row,
+    two rows and around one 64-row chunk (bare key and value columns: no
+    projections; the sort skipped for a single row)."""
+    monkeypatch.setenv("WARPDB_GROUP_ROWS", "general")
+    rng = np.random.default_rng(rows)
+    cols = {"price": spread_values(rng, rows), "quantity": rng.integers(-3, 3, rows).astype(np.int32) * 5000}
+    g, k, s, c = run(cols, None, 64)
+    rk, rs, rc = ora.group_sum(ora.HostTable(cols), "price", "quantity", capacity=64)
+    assert g == len(rk) and np.array_equal(k, rk) and np.array_equal(c, rc)
+    assert np.array_equal(bits(s), bits(rs))
